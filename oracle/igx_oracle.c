@@ -1,0 +1,575 @@
+/*
+ * igx_oracle.c -- CPU restatement of Inspektor Gadget's event-aggregation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (`inspektor-gadget_amd/`) links or
+ * calls this file; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * load it (as the checker / CPU baseline), never as the thing measured or shipped.
+ *
+ * The reference path is Go (+ eBPF C) and cannot be built in this image (no Go
+ * toolchain), so this is a restatement, pinned by the reference's own
+ * table tests re-encoded under tests/golden/ (see tests/test_oracle_golden.py).
+ *
+ * Every function cites the reference file:line it restates (paths relative to the
+ * reference repository root).
+ *
+ * Contents
+ *   1. counter-based synthetic event generators (shared bit-exactly with the GPU
+ *      generator kernels in csrc/k_gen.hip; not a reference algorithm)
+ *   2. filter predicate evaluation        pkg/columns/filter/filter.go:187-325
+ *   3. Go 1.19 sort.SliceStable restatement (stable_func / insertionSort_func /
+ *      symMerge_func / rotate_func; stdlib, transliterated in SURVEY.md App. C) driven by
+ *      getLessFunc                         pkg/columns/sort/sort.go:35-83,125-135
+ *   4. keyed aggregation with first-occurrence ("Go map + BPF hash") semantics
+ *      pkg/gadgets/top/tcp/tracer/bpf/tcptop.bpf.c:33-110
+ *      pkg/gadgets/top/file/tracer/bpf/filetop.bpf.c:39-94
+ *      pkg/gadgets/top/block-io/tracer/bpf/biotop.bpf.c:85-130
+ *      pkg/gadgets/trace/network/tracer/bpf/graph.c:102-114 (distinct insert)
+ *   5. log2 latency histograms           pkg/gadgets/profile/block-io/tracer/bpf/biolatency.bpf.c:100-154
+ *                                        pkg/gadgets/profile/block-io/tracer/bpf/bits.bpf.h:8-29
+ *   6. the top-tcp CPU path as the reference runs it (map group-by -> SortEntries ->
+ *      truncate), used as the CPU baseline ("port") in bench.py
+ *      pkg/gadgets/top/tcp/tracer/tracer.go:147-253, pkg/gadgets/top/top.go:39-41
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+typedef uint8_t u8;
+typedef int64_t i64;
+
+/* ------------------------------------------------------------------------------------
+ * 1. Synthetic generators (counter-based: event i's fields depend only on (seed, i)).
+ * ---------------------------------------------------------------------------------- */
+static inline u64 sm64(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+/* stream-separated counter RNG; identical formula in csrc/k_gen.hip */
+static inline u64 rnd(u64 seed, u64 stream, u64 i) {
+    return sm64(sm64(seed ^ (stream * 0xD1B54A32D192ED03ull)) ^ (i * 0x9E3779B97F4A7C15ull));
+}
+/* lower_bound over u63 CDF thresholds (last threshold == 1<<63) */
+static inline u64 cdf_pick(const u64 *cdf, u64 n, u64 r) {
+    u64 u = r >> 1, lo = 0, hi = n - 1;
+    while (lo < hi) {
+        u64 mid = (lo + hi) >> 1;
+        if (u < cdf[mid]) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+/* C2 top-tcp stream.  Key universe of G keys per rank (ingest-partitioned), Zipf over
+ * key rank via cdf.  Fields mirror ip_key_t (tcptop.h:8-17) in SoA form. */
+void or_gen_tcp(u64 seed, u64 rank, u64 G, u64 permA, u64 permB, const u64 *cdf,
+                u64 base, u64 n, u8 *saddr, u8 *daddr, u64 *mntns, u32 *pid, u8 *comm,
+                u16 *lport, u16 *dport, u16 *family, u32 *size, u8 *dir) {
+    static const char *names[8] = {"nginx", "curl", "postgres", "redis-server",
+                                   "java", "python3", "envoy", "node"};
+    static const u16 ports[8] = {80, 443, 8080, 53, 3306, 6379, 5432, 9092};
+    for (u64 j = 0; j < n; j++) {
+        u64 i = base + j;
+        u64 r = cdf_pick(cdf, G, rnd(seed, 1, i));
+        u64 kid = (r * permA + permB) % G;            /* scrambled local key id */
+        u64 gk = kid * 64 + rank;                       /* globally unique key id */
+        u64 p = 1000 + (gk >> 4);                        /* 16 keys per pid */
+        u64 hp = sm64(p ^ 0x5EED);
+        u64 hk = sm64(gk ^ 0xFACE);
+        u8 *sa = saddr + 16 * j, *da = daddr + 16 * j, *cm = comm + 16 * j;
+        memset(sa, 0, 16); memset(da, 0, 16); memset(cm, 0, 16);
+        u16 fam = (hk % 10 == 0) ? 10 : 2;
+        u8 s4[4] = {10, 0, (u8)(hp >> 8), (u8)hp};
+        u8 d4[4] = {10, (u8)(1 + ((hk >> 40) & 7)), (u8)(hk >> 16), (u8)(hk >> 24)};
+        if (fam == 2) {
+            memcpy(sa, s4, 4); memcpy(da, d4, 4);
+        } else {
+            sa[10] = sa[11] = 0xff; memcpy(sa + 12, s4, 4);
+            da[10] = da[11] = 0xff; memcpy(da + 12, d4, 4);
+        }
+        mntns[j] = 4026531840ull + ((hp >> 20) & 63);
+        pid[j] = (u32)p;
+        const char *nm = names[(hp >> 32) & 7];
+        size_t L = strlen(nm);
+        memcpy(cm, nm, L);
+        cm[L] = (u8)('a' + ((hp >> 40) & 31) % 26);   /* 8 names x 26 suffixes */
+        lport[j] = (u16)(1024 + (gk & 15) + 16 * ((hk >> 8) % 2048));
+        dport[j] = ports[(hk >> 48) & 7];
+        family[j] = fam;
+        u64 e = rnd(seed, 2, i);
+        dir[j] = (u8)(e & 1);
+        size[j] = (u32)(1 + (e >> 8) % 65535);
+    }
+}
+
+/* C1 trace-open stream (pkg/gadgets/trace/open/types/types.go:22-33 fields).  comm is
+ * drawn from a 64-name dictionary with Zipf s=1.0 via comm_cdf (64 thresholds). */
+void or_gen_open(u64 seed, const u64 *comm_cdf, u64 base, u64 n, u32 *pid, u32 *uid,
+                 u64 *mntns, u8 *comm, i64 *ret, i64 *fd, i64 *err, u32 *path_id) {
+    for (u64 j = 0; j < n; j++) {
+        u64 i = base + j;
+        u64 a = rnd(seed, 1, i), b = rnd(seed, 2, i), c = rnd(seed, 3, i);
+        pid[j] = (u32)(1 + a % 32767);
+        u64 ur = (a >> 32) % 11;
+        uid[j] = ur == 0 ? 0 : (u32)(999 + ur);
+        mntns[j] = 4026531840ull + ((a >> 40) & 15);
+        u64 k = cdf_pick(comm_cdf, 64, b);
+        u8 *cm = comm + 16 * j;
+        memset(cm, 0, 16);
+        /* name = "proc" + 2 hex-ish letters, <= 15 chars, no NUL */
+        static const char *stem[8] = {"bash", "sshd", "containerd", "kubelet", "cat",
+                                      "systemd-journal", "runc", "ls"};
+        const char *s = stem[k & 7];
+        size_t L = strlen(s);
+        if (L > 13) L = 13;
+        memcpy(cm, s, L);
+        cm[L] = (u8)('a' + (k >> 3));
+        i64 r;
+        if (c % 10 == 0) r = -(i64)(1 + (c >> 8) % 13);
+        else r = (i64)(3 + (c >> 8) % 1021);
+        ret[j] = r;
+        fd[j] = r >= 0 ? r : 0;
+        err[j] = r < 0 ? -r : 0;
+        path_id[j] = (u32)((c >> 32) & 4095);
+    }
+}
+
+/* C3 block-io completions: dev (MKDEV(8, 16k), biolatency.h:8-11), container dictionary
+ * id, delta_ns from a discretised lognormal quantile table q (nq+1 entries). */
+void or_gen_bio(u64 seed, const u64 *q, u64 nq, u64 base, u64 n, u32 *dev, u32 *cont,
+                u64 *delta) {
+    for (u64 j = 0; j < n; j++) {
+        u64 i = base + j;
+        u64 a = rnd(seed, 1, i), b = rnd(seed, 2, i);
+        dev[j] = (8u << 20) | (u32)(16 * (a & 15));
+        cont[j] = (u32)((a >> 8) & 255);
+        u64 idx = (b >> 32) % nq;
+        u64 lo = q[idx], hi = q[idx + 1];
+        delta[j] = lo + (b & 0xffffffffull) % (hi - lo + 1);
+    }
+}
+
+/* C4 network events (advisor.go:277-320 inputs as dictionary ids). */
+void or_gen_np(u64 seed, u64 nsrc, u64 npeer_total, u64 base, u64 n, u32 *src, u32 *peer,
+               u16 *port, u8 *pkt, u8 *typ, u8 *proto, u32 *hostip, u32 *raddr) {
+    static const u16 ports[8] = {80, 443, 53, 8080, 5432, 6379, 9090, 3000};
+    for (u64 j = 0; j < n; j++) {
+        u64 i = base + j;
+        u64 a = rnd(seed, 1, i), b = rnd(seed, 2, i), c = rnd(seed, 3, i);
+        u32 s = (u32)(a % nsrc);
+        u64 slot = (a >> 32) & 63;                        /* one of 64 peers of src */
+        u32 pe = (u32)(sm64((u64)s * 64 + slot) % npeer_total);
+        src[j] = s;
+        peer[j] = pe;
+        port[j] = ports[(b >> 8) & 7];
+        u64 pk = b % 100;
+        pkt[j] = pk < 60 ? 4 /*OUTGOING*/ : (pk < 95 ? 0 /*HOST*/ : 1 /*BROADCAST*/);
+        typ[j] = (c % 100 == 0) ? 1 : 0;                  /* 0 = normal */
+        proto[j] = (u8)((c >> 8) % 3 == 0 ? 17 : 6);
+        hostip[j] = 0x0a000000u | (u32)(s & 0xffff);
+        raddr[j] = ((c >> 16) % 100 == 0) ? hostip[j] : (0x0a600000u | (pe & 0xfffff));
+    }
+}
+
+/* C5 top-file stream: key file_id{inode,dev,pid,tid} (filetop.h:13-18). */
+void or_gen_file(u64 seed, u64 rank, u64 G, u64 permA, u64 permB, const u64 *cdf, u64 base,
+                 u64 n, u64 *inode, u32 *dev, u32 *pid, u32 *tid, u8 *op, u32 *count) {
+    for (u64 j = 0; j < n; j++) {
+        u64 i = base + j;
+        u64 r = cdf_pick(cdf, G, rnd(seed, 1, i));
+        u64 kid = (r * permA + permB) % G;
+        u64 gk = kid * 64 + rank;
+        u64 h = sm64(gk ^ 0xF11E);
+        inode[j] = sm64(gk ^ 0x9A7B);                     /* hash64(path) stand-in */
+        dev[j] = (u32)((8u << 20) | (u32)(h & 15));
+        pid[j] = (u32)(100 + (gk >> 3));
+        tid[j] = pid[j] + (u32)(gk & 7);
+        u64 e = rnd(seed, 2, i);
+        op[j] = (u8)(e & 1);                               /* 0 READ, 1 WRITE */
+        count[j] = (u32)(1 + (e >> 8) % ((1u << 20) - 1));
+    }
+}
+
+/* ------------------------------------------------------------------------------------
+ * 2. Filter predicates -- getComparisonFuncForComparisonType (filter.go:236-263):
+ *    result = (field OP ref) != negate; FilterSpecs.MatchAll (filter.go:266-273).
+ * ---------------------------------------------------------------------------------- */
+enum { OR_INT = 0, OR_UINT = 1, OR_FLOAT = 2, OR_BYTES = 3 };
+enum { OR_EQ = 0, OR_LT = 2, OR_LE = 3, OR_GT = 4, OR_GE = 5 };
+
+typedef struct {
+    const void *ptr;  /* column base */
+    u32 width;        /* bytes per row */
+    u32 kind;         /* OR_INT / OR_UINT / OR_FLOAT / OR_BYTES */
+    u32 op;           /* comparison */
+    u32 negate;
+    const u8 *ref;    /* reference value, `width` bytes (already Convert()-ed) */
+} or_pred;
+
+static int cmp_field(const or_pred *p, u64 row) {
+    const u8 *f = (const u8 *)p->ptr + (u64)p->width * row;
+    if (p->kind == OR_BYTES) {
+        int c = memcmp(f, p->ref, p->width);   /* Go string compare == bytewise unsigned */
+        return c < 0 ? -1 : (c > 0);
+    }
+    if (p->kind == OR_FLOAT) {
+        double a, b;
+        if (p->width == 4) { float x, y; memcpy(&x, f, 4); memcpy(&y, p->ref, 4); a = x; b = y; }
+        else { memcpy(&a, f, 8); memcpy(&b, p->ref, 8); }
+        if (a != a || b != b) return 2;          /* unordered: every comparison false */
+        return a < b ? -1 : (a > b);
+    }
+    if (p->kind == OR_INT) {
+        i64 a = 0, b = 0;
+        switch (p->width) {
+        case 1: a = *(const int8_t *)f; b = *(const int8_t *)p->ref; break;
+        case 2: { int16_t x, y; memcpy(&x, f, 2); memcpy(&y, p->ref, 2); a = x; b = y; } break;
+        case 4: { int32_t x, y; memcpy(&x, f, 4); memcpy(&y, p->ref, 4); a = x; b = y; } break;
+        default: memcpy(&a, f, 8); memcpy(&b, p->ref, 8);
+        }
+        return a < b ? -1 : (a > b);
+    }
+    u64 a = 0, b = 0;
+    memcpy(&a, f, p->width); memcpy(&b, p->ref, p->width);
+    return a < b ? -1 : (a > b);
+}
+
+static int pred_match(const or_pred *p, u64 row) {
+    int c = cmp_field(p, row), r;
+    if (c == 2) r = 0;
+    else switch (p->op) {
+        case OR_EQ: r = c == 0; break;
+        case OR_LT: r = c < 0; break;
+        case OR_LE: r = c <= 0; break;
+        case OR_GT: r = c > 0; break;
+        case OR_GE: r = c >= 0; break;
+        default: r = 0;
+    }
+    return r != (int)p->negate;
+}
+
+/* FilterEntries (filter.go:294-325): order-preserving selection; nil rows (valid[i]==0)
+ * are skipped.  Returns count written to out_idx. */
+u64 or_filter(const or_pred *preds, u32 npred, const u8 *valid, u64 n, u32 *out_idx) {
+    u64 k = 0;
+    for (u64 i = 0; i < n; i++) {
+        if (valid && !valid[i]) continue;
+        int ok = 1;
+        for (u32 p = 0; p < npred && ok; p++) ok = pred_match(&preds[p], i);
+        if (ok) out_idx[k++] = (u32)i;
+    }
+    return k;
+}
+
+/* ------------------------------------------------------------------------------------
+ * 3. Go 1.19 sort.SliceStable restatement.  `less(i,j)` and `swap` act on the live
+ *    permutation `perm` (an array of row ids, the analogue of []*T).
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+    const void *ptr;   /* column base, indexed by row id */
+    u32 width, kind, desc;
+} or_sortkey;
+
+typedef struct {
+    u32 *perm;
+    const u8 *valid;     /* nil entries (valid==0) sort last (sort.go:127-132) */
+    const or_sortkey *key;
+} less_ctx;
+
+static int col_lt(const or_sortkey *k, u32 a, u32 b) {
+    const u8 *fa = (const u8 *)k->ptr + (u64)k->width * a;
+    const u8 *fb = (const u8 *)k->ptr + (u64)k->width * b;
+    if (k->kind == OR_BYTES) return memcmp(fa, fb, k->width) < 0;
+    if (k->kind == OR_FLOAT) {
+        if (k->width == 4) { float x, y; memcpy(&x, fa, 4); memcpy(&y, fb, 4); return x < y; }
+        double x, y; memcpy(&x, fa, 8); memcpy(&y, fb, 8); return x < y;
+    }
+    if (k->kind == OR_INT) {
+        i64 x = 0, y = 0;
+        switch (k->width) {
+        case 1: x = *(const int8_t *)fa; y = *(const int8_t *)fb; break;
+        case 2: { int16_t p, q; memcpy(&p, fa, 2); memcpy(&q, fb, 2); x = p; y = q; } break;
+        case 4: { int32_t p, q; memcpy(&p, fa, 4); memcpy(&q, fb, 4); x = p; y = q; } break;
+        default: memcpy(&x, fa, 8); memcpy(&y, fb, 8);
+        }
+        return x < y;
+    }
+    u64 x = 0, y = 0;
+    memcpy(&x, fa, k->width); memcpy(&y, fb, k->width);
+    return x < y;
+}
+
+/* getLessFunc (sort.go:125-135): !(a<b) != order, OrderAsc=true (types.go:37-38) */
+static inline int go_less(const less_ctx *c, u64 i, u64 j) {
+    u32 a = c->perm[i], b = c->perm[j];
+    if (c->valid && !c->valid[a]) return 0;
+    if (c->valid && !c->valid[b]) return 1;
+    int lt = col_lt(c->key, a, b);
+    int order_asc = !c->key->desc;
+    return (!lt) != order_asc;
+}
+static inline void go_swap(const less_ctx *c, u64 i, u64 j) {
+    u32 t = c->perm[i]; c->perm[i] = c->perm[j]; c->perm[j] = t;
+}
+static void insertion_sort(const less_ctx *c, u64 a, u64 b) {
+    for (u64 i = a + 1; i < b; i++)
+        for (u64 j = i; j > a && go_less(c, j, j - 1); j--) go_swap(c, j, j - 1);
+}
+static void swap_range(const less_ctx *c, u64 a, u64 b, u64 n) {
+    for (u64 i = 0; i < n; i++) go_swap(c, a + i, b + i);
+}
+static void rotate(const less_ctx *c, u64 a, u64 m, u64 b) {
+    u64 i = m - a, j = b - m;
+    while (i != j) {
+        if (i > j) { swap_range(c, m - i, m, j); i -= j; }
+        else { swap_range(c, m - i, m + j - i, i); j -= i; }
+    }
+    swap_range(c, m - i, m, i);
+}
+static void sym_merge(const less_ctx *c, u64 a, u64 m, u64 b) {
+    if (m - a == 1) {
+        u64 i = m, j = b;
+        while (i < j) { u64 h = (i + j) >> 1; if (go_less(c, h, a)) i = h + 1; else j = h; }
+        for (u64 k = a; k + 1 < i; k++) go_swap(c, k, k + 1);
+        return;
+    }
+    if (b - m == 1) {
+        u64 i = a, j = m;
+        while (i < j) { u64 h = (i + j) >> 1; if (!go_less(c, m, h)) i = h + 1; else j = h; }
+        for (u64 k = m; k > i; k--) go_swap(c, k, k - 1);
+        return;
+    }
+    u64 mid = (a + b) >> 1, n = mid + m, start, r;
+    if (m > mid) { start = n - b; r = mid; } else { start = a; r = m; }
+    u64 p = n - 1;
+    while (start < r) {
+        u64 cc = (start + r) >> 1;
+        if (!go_less(c, p - cc, cc)) start = cc + 1; else r = cc;
+    }
+    u64 end = n - start;
+    if (start < m && m < end) rotate(c, start, m, end);
+    if (a < start && start < mid) sym_merge(c, a, start, mid);
+    if (mid < end && end < b) sym_merge(c, mid, end, b);
+}
+static void go_stable(const less_ctx *c, u64 n) {
+    u64 bs = 20, a = 0, b = bs;
+    while (b <= n) { insertion_sort(c, a, b); a = b; b += bs; }
+    insertion_sort(c, a, n);
+    while (bs < n) {
+        a = 0; b = 2 * bs;
+        while (b <= n) { sym_merge(c, a, a + bs, b); a = b; b += 2 * bs; }
+        if (a + bs < n) sym_merge(c, a, a + bs, n);
+        bs *= 2;
+    }
+}
+
+/* ColumnSorterCollection.Sort (sort.go:35-83): keys given in sortBy order (first =
+ * highest priority); one stable pass per key, last key first (Prepare reverses, :91). */
+void or_sort_entries(u32 *perm, u64 n, const u8 *valid, const or_sortkey *keys, u32 nkeys) {
+    if (n == 0) return;
+    for (int k = (int)nkeys - 1; k >= 0; k--) {
+        less_ctx c = {perm, valid, &keys[k]};
+        go_stable(&c, n);
+    }
+}
+
+/* ------------------------------------------------------------------------------------
+ * 4. Keyed aggregation (Go-map / BPF-hash semantics, canonical first-occurrence order).
+ *    Rows are (packed key bytes, aggregate inputs).  Each aggregate is
+ *      COUNT  (cond?): += 1
+ *      SUM    (cond?): += value
+ *    wrapped to out_width bytes (group.go:137-151 SetInt wraps; BPF u32 io++ wraps).
+ *    Groups are emitted in first-occurrence order with their first row index.
+ * ---------------------------------------------------------------------------------- */
+enum { OR_AGG_COUNT = 0, OR_AGG_SUM = 1 };
+typedef struct {
+    u32 kind;
+    u32 val_width;       /* bytes of the value column (SUM) */
+    const void *val;     /* value column (SUM) */
+    u32 cond_width;      /* 0 = unconditional */
+    const void *cond;    /* condition column */
+    u64 cond_val;        /* row counts iff cond == cond_val */
+    u32 out_width;       /* wrap width in bytes (1,2,4,8) */
+} or_agg;
+
+static inline u64 ld_u(const void *p, u32 w, u64 row) {
+    const u8 *q = (const u8 *)p + (u64)w * row;
+    u64 v = 0; memcpy(&v, q, w); return v;
+}
+static inline u64 fnv(const u8 *k, u32 n) {
+    u64 h = 1469598103934665603ull;
+    for (u32 i = 0; i < n; i++) { h ^= k[i]; h *= 1099511628211ull; }
+    return h ^ (h >> 29);
+}
+
+typedef struct {
+    u64 cap, mask, n;
+    u32 kb;
+    u32 *slot;          /* group id + 1, 0 = empty */
+    u64 *hash;
+} or_map;
+
+static int map_init(or_map *m, u64 expect, u32 kb) {
+    u64 cap = 16;
+    while (cap < expect * 2) cap <<= 1;
+    m->cap = cap; m->mask = cap - 1; m->n = 0; m->kb = kb;
+    m->slot = (u32 *)calloc(cap, sizeof(u32));
+    m->hash = (u64 *)malloc(cap * sizeof(u64));
+    return m->slot && m->hash ? 0 : -1;
+}
+static void map_free(or_map *m) { free(m->slot); free(m->hash); }
+
+/* returns group id; *is_new set when inserted. keys_out grows as groups are added. */
+static u64 map_find_or_insert(or_map *m, const u8 *key, u8 *keys_out, int *is_new) {
+    u64 h = fnv(key, m->kb), s = h & m->mask;
+    for (;;) {
+        u32 g = m->slot[s];
+        if (!g) {
+            u64 id = m->n++;
+            m->slot[s] = (u32)(id + 1);
+            m->hash[s] = h;
+            memcpy(keys_out + (u64)m->kb * id, key, m->kb);
+            *is_new = 1;
+            return id;
+        }
+        if (m->hash[s] == h && memcmp(keys_out + (u64)m->kb * (g - 1), key, m->kb) == 0) {
+            *is_new = 0;
+            return g - 1;
+        }
+        s = (s + 1) & m->mask;
+    }
+}
+
+/* Generic group-by over rows [0,n) of a packed key matrix `keys` (n x kb bytes).  Rows
+ * with valid==0 are skipped (nil / filtered).  Outputs: out_keys (G x kb), out_aggs
+ * (naggs x maxG, u64 each, column-major), out_first (row index).  Returns G, or
+ * (u64)-1 if maxG is exceeded. */
+u64 or_groupby(const u8 *keys, u32 kb, u64 n, const u8 *valid, const or_agg *aggs,
+               u32 naggs, u64 base_idx, u64 maxG, u8 *out_keys, u64 *out_aggs,
+               u64 *out_first) {
+    or_map m;
+    if (map_init(&m, maxG, kb)) return (u64)-1;
+    for (u64 i = 0; i < n; i++) {
+        if (valid && !valid[i]) continue;
+        int is_new;
+        if (m.n >= maxG) {
+            /* probe only: a new key would overflow */
+        }
+        u64 g = map_find_or_insert(&m, keys + (u64)kb * i, out_keys, &is_new);
+        if (g >= maxG) { map_free(&m); return (u64)-1; }
+        if (is_new) {
+            out_first[g] = base_idx + i;
+            for (u32 a = 0; a < naggs; a++) out_aggs[(u64)a * maxG + g] = 0;
+        }
+        for (u32 a = 0; a < naggs; a++) {
+            const or_agg *A = &aggs[a];
+            if (A->cond_width && ld_u(A->cond, A->cond_width, i) != A->cond_val) continue;
+            u64 add = A->kind == OR_AGG_COUNT ? 1 : ld_u(A->val, A->val_width, i);
+            u64 *dst = &out_aggs[(u64)a * maxG + g];
+            u64 v = *dst + add;
+            if (A->out_width < 8) v &= (1ull << (8 * A->out_width)) - 1;
+            *dst = v;
+        }
+    }
+    u64 G = m.n;
+    map_free(&m);
+    return G;
+}
+
+/* ------------------------------------------------------------------------------------
+ * 5. log2 histograms -- bits.bpf.h:8-29 (log2 / log2l), biolatency.bpf.c:114-149:
+ *    delta<0 -> skipped; v = delta / divisor (1000 usecs, 1e6 msecs); slot = log2l(v),
+ *    clamped to MAX_SLOTS-1 = 26; slots are u32 (__sync_fetch_and_add wraps).
+ * ---------------------------------------------------------------------------------- */
+static inline u64 bpf_log2(u32 v) {
+    u32 shift, r;
+    r = (v > 0xFFFF) << 4; v >>= r;
+    shift = (v > 0xFF) << 3; v >>= shift; r |= shift;
+    shift = (v > 0xF) << 2; v >>= shift; r |= shift;
+    shift = (v > 0x3) << 1; v >>= shift; r |= shift;
+    r |= (v >> 1);
+    return r;
+}
+u64 or_log2l(u64 v) {
+    u32 hi = (u32)(v >> 32);
+    if (hi) return bpf_log2(hi) + 32;
+    return bpf_log2((u32)v);
+}
+
+/* key = dev_index(dev) * ncont + cont; dev_index via the sorted dev table `devs`.
+ * hist is nkeys x nslots u32, accumulated (not cleared). delta is s64 (signed). */
+void or_hist_log2(const u32 *dev, const u32 *cont, const i64 *delta, u64 n, const u32 *devs,
+                  u32 ndev, u32 ncont, u64 divisor, u32 nslots, u32 *hist) {
+    for (u64 i = 0; i < n; i++) {
+        i64 d = delta[i];
+        if (d < 0) continue;
+        u32 di = 0;
+        while (di < ndev && devs[di] != dev[i]) di++;
+        if (di == ndev) continue;                    /* unknown device: not counted */
+        u64 v = (u64)d / divisor;
+        u64 slot = or_log2l(v);
+        if (slot >= nslots) slot = nslots - 1;
+        u64 key = (u64)di * ncont + cont[i];
+        hist[key * nslots + slot] += 1;
+    }
+}
+
+/* ------------------------------------------------------------------------------------
+ * 6. top-tcp CPU path as the reference runs it, for timing (the "port" CPU baseline):
+ *    probe_ip per event (tcptop.bpf.c:83-107: build ip_key_t, lookup-or-insert, +=),
+ *    nextStats (tracer.go:147-226: one Stats per map entry), top.SortStats ->
+ *    SortEntries(["-sent","-recv"]) (top.go:39-41, sort.go:35-83), truncate to
+ *    max-rows (tracer.go:249-253).  Canonical pre-sort order = first occurrence.
+ *    Returns the number of groups; out_* receive the first `k` sorted rows.
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+    u8 saddr[16], daddr[16];
+    u64 mntns;
+    u32 pid;
+    u8 name[16];
+    u16 lport, dport, family;
+    u16 pad;
+} ip_key_t;  /* 72 bytes; tcptop.h:8-17 */
+
+u64 or_top_tcp(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 *pid,
+               const u8 *comm, const u16 *lport, const u16 *dport, const u16 *family,
+               const u32 *size, const u8 *dir, u64 n, u64 base_idx, u64 maxG, u32 k,
+               u8 *out_keys /* k x 72 */, u64 *out_sent, u64 *out_recv, u64 *out_first) {
+    or_map m;
+    if (map_init(&m, maxG, sizeof(ip_key_t))) return (u64)-1;
+    u8 *keys = (u8 *)malloc(maxG * sizeof(ip_key_t));
+    u64 *sent = (u64 *)malloc(maxG * 8), *recv = (u64 *)malloc(maxG * 8);
+    u64 *first = (u64 *)malloc(maxG * 8);
+    ip_key_t key;
+    for (u64 i = 0; i < n; i++) {
+        if (family[i] != 2 && family[i] != 10) continue;   /* tcptop.bpf.c:54-55 */
+        memset(&key, 0, sizeof key);
+        memcpy(key.saddr, saddr + 16 * i, 16);
+        memcpy(key.daddr, daddr + 16 * i, 16);
+        key.mntns = mntns[i]; key.pid = pid[i];
+        memcpy(key.name, comm + 16 * i, 16);
+        key.lport = lport[i]; key.dport = dport[i]; key.family = family[i];
+        int is_new;
+        u64 g = map_find_or_insert(&m, (const u8 *)&key, keys, &is_new);
+        if (g >= maxG) { g = (u64)-1; break; }
+        if (is_new) { sent[g] = recv[g] = 0; first[g] = base_idx + i; }
+        if (dir[i]) recv[g] += size[i]; else sent[g] += size[i];
+    }
+    u64 G = m.n;
+    map_free(&m);
+    /* []*Stats in canonical order, then SortEntries(-sent,-recv) */
+    u32 *perm = (u32 *)malloc((G ? G : 1) * sizeof(u32));
+    for (u64 g = 0; g < G; g++) perm[g] = (u32)g;
+    or_sortkey ks[2] = {{sent, 8, OR_UINT, 1}, {recv, 8, OR_UINT, 1}};
+    or_sort_entries(perm, G, NULL, ks, 2);
+    for (u32 r = 0; r < k && r < G; r++) {
+        u32 g = perm[r];
+        memcpy(out_keys + 72ull * r, keys + 72ull * g, 72);
+        out_sent[r] = sent[g]; out_recv[r] = recv[g]; out_first[r] = first[g];
+    }
+    free(perm); free(keys); free(sent); free(recv); free(first);
+    return G;
+}

@@ -1,0 +1,677 @@
+"""CPU oracle for the igx event-aggregation path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module.  The product package (``inspektor-gadget_amd``) never imports it.
+
+Two halves:
+
+* ctypes bindings to ``liboracle.so`` (``igx_oracle.c``): bulk integer work -- filter
+  evaluation, Go ``sort.SliceStable`` restatement, keyed aggregation, log2 histograms,
+  synthetic generators -- fast enough for parity at 1M-10M rows.
+* pure-Python restatements of the small, string-heavy reference logic:
+  ``GetFilterFromString`` parsing (pkg/columns/filter/filter.go:53-172),
+  ``GroupEntries`` (pkg/columns/group/group.go:27-165), the Go stable sort on tiny inputs
+   and the closed-form tie order, ``getReport``
+  (pkg/gadgets/profile/block-io/tracer/tracer.go:56-90) and the network-policy advisor
+  (pkg/gadgets/advise/networkpolicy/advisor/advisor.go:100-387).
+
+Pinning: every restatement here is checked against the reference's own table tests and
+golden files re-encoded under ``tests/golden`` (tests/test_oracle_golden.py).  The DESC
+tie order of the Go stdlib sort is pinned only by the transliteration itself ("parity
+unpinned" at the Go-stdlib boundary).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import re
+import subprocess
+import struct
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else C.c_void_p(0)
+
+
+def _declare(L):
+    u64, vp = C.c_uint64, C.c_void_p
+    L.or_gen_tcp.argtypes = [u64] * 5 + [vp, u64, u64] + [vp] * 10
+    L.or_gen_open.argtypes = [u64, vp, u64, u64] + [vp] * 8
+    L.or_gen_bio.argtypes = [u64, vp, u64, u64, u64, vp, vp, vp]
+    L.or_gen_np.argtypes = [u64, u64, u64, u64, u64] + [vp] * 8
+    L.or_gen_file.argtypes = [u64] * 5 + [vp, u64, u64] + [vp] * 6
+    L.or_filter.argtypes = [vp, C.c_uint32, vp, u64, vp]
+    L.or_filter.restype = u64
+    L.or_sort_entries.argtypes = [vp, u64, vp, vp, C.c_uint32]
+    L.or_groupby.argtypes = [vp, C.c_uint32, u64, vp, vp, C.c_uint32, u64, u64, vp, vp, vp]
+    L.or_groupby.restype = u64
+    L.or_log2l.argtypes = [u64]
+    L.or_log2l.restype = u64
+    L.or_hist_log2.argtypes = [vp, vp, vp, u64, vp, C.c_uint32, C.c_uint32, u64,
+                               C.c_uint32, vp]
+    L.or_top_tcp.argtypes = [vp] * 10 + [u64, u64, u64, C.c_uint32, vp, vp, vp, vp]
+    L.or_top_tcp.restype = u64
+
+
+# ------------------------------------------------------------------------------------
+# column vocabulary (Go reflect kinds -> width/class)
+# ------------------------------------------------------------------------------------
+KIND_CLASS = {
+    "int": ("int", 8), "int8": ("int", 1), "int16": ("int", 2), "int32": ("int", 4),
+    "int64": ("int", 8), "uint": ("uint", 8), "uint8": ("uint", 1), "uint16": ("uint", 2),
+    "uint32": ("uint", 4), "uint64": ("uint", 8), "float32": ("float", 4),
+    "float64": ("float", 8), "string": ("string", None), "bool": ("bool", 1),
+    "struct": ("struct", 0),
+}
+CLASS_CODE = {"int": 0, "uint": 1, "float": 2, "string": 3}
+OPS = {"eq": 0, "lt": 2, "le": 3, "gt": 4, "ge": 5}
+
+
+@dataclass
+class OCol:
+    name: str
+    kind: str            # reflect kind name, e.g. "int8", "string"
+    width: int = 0       # bytes per row in the SoA batch (strings: fixed width)
+    virtual: bool = False
+    extractor: bool = False
+
+
+class FilterError(Exception):
+    pass
+
+
+@dataclass
+class OPred:
+    col: OCol
+    op: str
+    negate: bool
+    ref: bytes = b""
+    regex: object = None
+
+
+def _parse_int(s: str, bits=64):
+    # strconv.ParseInt(s, 10, 64): optional sign, decimal digits only, range-checked
+    if not re.fullmatch(r"[+-]?[0-9]+", s):
+        raise ValueError(s)
+    v = int(s, 10)
+    if not (-(1 << 63) <= v < (1 << 63)):
+        raise ValueError(s)
+    return v
+
+
+def _parse_uint(s: str):
+    # strconv.ParseUint(s, 10, 64): no sign, decimal digits only
+    if not re.fullmatch(r"[0-9]+", s):
+        raise ValueError(s)
+    v = int(s, 10)
+    if v >= (1 << 64):
+        raise ValueError(s)
+    return v
+
+
+def _parse_float(s: str):
+    # strconv.ParseFloat(s, 64) (decimal / exponent / inf / nan forms)
+    t = s.lower()
+    if t in ("inf", "+inf", "infinity", "+infinity"):
+        return math.inf
+    if t in ("-inf", "-infinity"):
+        return -math.inf
+    if t == "nan":
+        return math.nan
+    if not re.fullmatch(r"[+-]?(\d+\.?\d*|\.\d+)(e[+-]?\d+)?", t):
+        raise ValueError(s)
+    return float(t)
+
+
+def parse_filter(cols: dict, filt: str) -> OPred:
+    """GetFilterFromString (filter.go:91-172) + getValueFromFilterSpec (:53-87)."""
+    info = filt.split(":", 1)
+    if len(info) == 1:
+        info.append("")                                   # :93-96
+    col = cols.get(info[0].lower())                       # columns.go:84 lower-cases
+    if col is None:
+        raise FilterError(f'could not apply filter: column "{info[0]}" not found')
+    rule = info[1]
+    negate = False
+    if rule.startswith("!"):                              # :113-117
+        negate = True
+        rule = rule[1:]
+    op = "eq"
+    regex = None
+    if rule.startswith("~"):                              # :119-127
+        op = "regex"
+        rule = rule[1:]
+        try:
+            regex = re.compile(rule)
+        except re.error as e:
+            raise FilterError(f"could not compile regular expression {rule!r}: {e}")
+    elif rule.startswith(">="):
+        op, rule = "ge", rule[2:]
+    elif rule.startswith(">"):
+        op, rule = "gt", rule[1:]
+    elif rule.startswith("<="):
+        op, rule = "le", rule[2:]
+    elif rule.startswith("<"):
+        op, rule = "lt", rule[1:]
+    cls, w = KIND_CLASS[col.kind]
+    if op == "regex":
+        if cls != "string":                               # :146-148
+            raise FilterError(f'tried to apply regular expression on non-string column "{col.name}"')
+        return OPred(col, op, negate, regex=regex)
+    if cls == "int":
+        try:
+            v = _parse_int(rule)
+        except ValueError:
+            raise FilterError(f'tried to compare "{rule}" to int column "{col.name}"')
+        ref = (v & ((1 << (8 * w)) - 1)).to_bytes(w, "little")   # Convert() truncates
+    elif cls == "uint":
+        try:
+            v = _parse_uint(rule)
+        except ValueError:
+            raise FilterError(f'tried to compare "{rule}" to uint column "{col.name}"')
+        ref = (v & ((1 << (8 * w)) - 1)).to_bytes(w, "little")
+    elif cls == "float":
+        try:
+            v = _parse_float(rule)
+        except ValueError:
+            raise FilterError(f'tried to compare "{rule}" to float column "{col.name}"')
+        ref = struct.pack("<f" if w == 4 else "<d", v)
+    elif cls == "string":
+        b = rule.encode()
+        ref = b[: col.width].ljust(col.width, b"\0")
+        if len(b) > col.width:
+            # a reference longer than the fixed-width column: equality can never hold
+            ref = b
+    else:
+        raise FilterError(f'tried to match "{rule}" on unsupported column "{col.name}"')
+    return OPred(col, op, negate, ref=ref)
+
+
+class _CPred(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("kind", C.c_uint32),
+                ("op", C.c_uint32), ("negate", C.c_uint32), ("ref", C.c_void_p)]
+
+
+def match_rows(preds, batch: dict, valid=None):
+    """MatchAll over SoA rows (filter.go:266-273); FilterEntries order (:294-325).
+    Returns the selected row indices (np.uint32)."""
+    n = len(valid) if valid is not None else len(next(iter(batch.values())))
+    keep = np.ones(n, dtype=bool) if valid is None else valid.astype(bool).copy()
+    cpreds = []
+    refbufs = []
+    for p in preds:
+        col = batch[p.col.name]
+        if p.op == "regex":
+            sel = np.zeros(n, dtype=bool)
+            for i in range(n):
+                if keep[i]:
+                    s = bytes(col[i]).rstrip(b"\0").decode(errors="replace")
+                    sel[i] = (p.regex.search(s) is not None) != p.negate
+            keep &= sel
+            continue
+        cls, w = KIND_CLASS[p.col.kind]
+        if cls == "string" and len(p.ref) > p.col.width:
+            # longer reference than the column: compare as Go strings in Python
+            sel = np.zeros(n, dtype=bool)
+            for i in range(n):
+                s = bytes(col[i]).rstrip(b"\0")
+                c = (s > p.ref) - (s < p.ref)
+                r = {"eq": c == 0, "lt": c < 0, "le": c <= 0, "gt": c > 0, "ge": c >= 0}[p.op]
+                sel[i] = r != p.negate
+            keep &= sel
+            continue
+        rb = np.frombuffer(p.ref, dtype=np.uint8).copy()
+        refbufs.append(rb)
+        colc = np.ascontiguousarray(col)
+        refbufs.append(colc)
+        cpreds.append(_CPred(colc.ctypes.data, p.col.width if cls == "string" else w,
+                             CLASS_CODE[cls], OPS[p.op], int(p.negate), rb.ctypes.data))
+    arr = (_CPred * max(1, len(cpreds)))(*cpreds)
+    valid8 = keep.astype(np.uint8)
+    out = np.empty(n, dtype=np.uint32)
+    k = lib().or_filter(C.cast(arr, C.c_void_p), len(cpreds), _p(valid8), n, _p(out))
+    return out[:k]
+
+
+# ------------------------------------------------------------------------------------
+# sort
+# ------------------------------------------------------------------------------------
+class _CSortKey(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("kind", C.c_uint32),
+                ("desc", C.c_uint32)]
+
+
+def go_sort_entries(keys, n, valid=None, perm=None):
+    """SortEntries via the Go 1.19 SliceStable restatement (C).  keys = list of
+    (np column indexed by row id, kind, desc) in sortBy order.  Returns the permutation
+    (row ids in output order) starting from `perm` (default identity)."""
+    perm = np.arange(n, dtype=np.uint32) if perm is None else np.array(perm, dtype=np.uint32)
+    ks, hold = [], []
+    for colarr, kind, desc in keys:
+        cls, w = KIND_CLASS[kind]
+        a = np.ascontiguousarray(colarr)
+        hold.append(a)
+        width = a.shape[1] if cls == "string" else w
+        ks.append(_CSortKey(a.ctypes.data, width, CLASS_CODE[cls], int(desc)))
+    arr = (_CSortKey * max(1, len(ks)))(*ks)
+    v8 = None if valid is None else np.ascontiguousarray(valid.astype(np.uint8))
+    lib().or_sort_entries(_p(perm), len(perm), _p(v8), C.cast(arr, C.c_void_p), len(ks))
+    return perm
+
+
+def go_slice_stable_py(data: list, less):
+    """Pure-Python transliteration of Go 1.19 sort.SliceStable;
+    `less(i, j)` reads the live list.  For small inputs only."""
+    n = len(data)
+
+    def swap(i, j):
+        data[i], data[j] = data[j], data[i]
+
+    def insertion(a, b):
+        for i in range(a + 1, b):
+            j = i
+            while j > a and less(j, j - 1):
+                swap(j, j - 1)
+                j -= 1
+
+    def swap_range(a, b, m):
+        for t in range(m):
+            swap(a + t, b + t)
+
+    def rotate(a, m, b):
+        i, j = m - a, b - m
+        while i != j:
+            if i > j:
+                swap_range(m - i, m, j)
+                i -= j
+            else:
+                swap_range(m - i, m + j - i, i)
+                j -= i
+        swap_range(m - i, m, i)
+
+    def sym_merge(a, m, b):
+        if m - a == 1:
+            i, j = m, b
+            while i < j:
+                h = (i + j) >> 1
+                if less(h, a):
+                    i = h + 1
+                else:
+                    j = h
+            for k in range(a, i - 1):
+                swap(k, k + 1)
+            return
+        if b - m == 1:
+            i, j = a, m
+            while i < j:
+                h = (i + j) >> 1
+                if not less(m, h):
+                    i = h + 1
+                else:
+                    j = h
+            for k in range(m, i, -1):
+                swap(k, k - 1)
+            return
+        mid = (a + b) >> 1
+        nn = mid + m
+        if m > mid:
+            start, r = nn - b, mid
+        else:
+            start, r = a, m
+        p = nn - 1
+        while start < r:
+            c = (start + r) >> 1
+            if not less(p - c, c):
+                start = c + 1
+            else:
+                r = c
+        end = nn - start
+        if start < m < end:
+            rotate(start, m, end)
+        if a < start < mid:
+            sym_merge(a, start, mid)
+        if mid < end < b:
+            sym_merge(mid, end, b)
+
+    bs, a, b = 20, 0, 20
+    while b <= n:
+        insertion(a, b)
+        a, b = b, b + bs
+    insertion(a, n)
+    while bs < n:
+        a, b = 0, 2 * bs
+        while b <= n:
+            sym_merge(a, a + bs, b)
+            a, b = b, b + 2 * bs
+        if a + bs < n:
+            sym_merge(a, a + bs, n)
+        bs *= 2
+    return data
+
+
+def go_sort_entries_py(rows: list, keys):
+    """SortEntries on a list of row values (None = nil entry) using the pure-Python Go
+    stable sort; keys = [(getter, desc)] in sortBy order (sort.go:35-135)."""
+    data = list(rows)
+    for getter, desc in reversed(keys):
+        def less(i, j, getter=getter, desc=desc):
+            if data[i] is None:
+                return False
+            if data[j] is None:
+                return True
+            return (not (getter(data[i]) < getter(data[j]))) != (not desc)
+        go_slice_stable_py(data, less)
+    return data
+
+
+def closed_form_perm(key_values, descs, n):
+    """SURVEY.md §0.3 closed form: effective direction of key i is desc_i XOR
+    (desc_1 ^ ... ^ desc_{i-1}); final tie-break is the pre-sort position, ascending
+    iff sum(desc) is even.  key_values: list of sequences of comparable python values."""
+    eff, par = [], 0
+    for d in descs:
+        eff.append(bool(d) ^ bool(par))
+        par ^= int(bool(d))
+
+    class K:
+        __slots__ = ("i",)
+
+        def __init__(self, i):
+            self.i = i
+
+        def __lt__(self, o):
+            for vals, e in zip(key_values, eff):
+                a, b = vals[self.i], vals[o.i]
+                if a != b:
+                    return (a > b) if e else (a < b)
+            return (self.i > o.i) if par else (self.i < o.i)
+
+    return sorted(range(n), key=K)
+
+
+# ------------------------------------------------------------------------------------
+# keyed aggregation / histograms
+# ------------------------------------------------------------------------------------
+class _CAgg(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("val_width", C.c_uint32), ("val", C.c_void_p),
+                ("cond_width", C.c_uint32), ("cond", C.c_void_p), ("cond_val", C.c_uint64),
+                ("out_width", C.c_uint32)]
+
+
+def groupby(keys_packed: np.ndarray, aggs, valid=None, base_idx=0, max_groups=None):
+    """Generic keyed aggregation in first-occurrence order.  keys_packed: (n, kb) uint8.
+    aggs: list of dicts {kind: 'count'|'sum', val: array|None, cond: array|None,
+    cond_val: int, out_width: int}.  Returns (keys (G,kb), aggs (naggs,G) u64, first)."""
+    keys_packed = np.ascontiguousarray(keys_packed, dtype=np.uint8)
+    n, kb = keys_packed.shape
+    maxG = max_groups or max(1, n)
+    cag, hold = [], []
+    for a in aggs:
+        val = a.get("val")
+        cond = a.get("cond")
+        if val is not None:
+            val = np.ascontiguousarray(val)
+            hold.append(val)
+        if cond is not None:
+            cond = np.ascontiguousarray(cond)
+            hold.append(cond)
+        cag.append(_CAgg(0 if a["kind"] == "count" else 1,
+                         0 if val is None else val.dtype.itemsize,
+                         0 if val is None else val.ctypes.data,
+                         0 if cond is None else cond.dtype.itemsize,
+                         0 if cond is None else cond.ctypes.data,
+                         int(a.get("cond_val", 0)), int(a.get("out_width", 8))))
+    arr = (_CAgg * max(1, len(cag)))(*cag)
+    out_keys = np.empty((maxG, kb), dtype=np.uint8)
+    out_aggs = np.zeros((max(1, len(aggs)), maxG), dtype=np.uint64)
+    out_first = np.empty(maxG, dtype=np.uint64)
+    v8 = None if valid is None else np.ascontiguousarray(valid.astype(np.uint8))
+    G = lib().or_groupby(_p(keys_packed), kb, n, _p(v8), C.cast(arr, C.c_void_p), len(cag),
+                         base_idx, maxG, _p(out_keys), _p(out_aggs), _p(out_first))
+    if G == (1 << 64) - 1:
+        raise RuntimeError("oracle groupby: too many groups")
+    return out_keys[:G], out_aggs[: len(aggs), :G], out_first[:G]
+
+
+def log2l(v: int) -> int:
+    return int(lib().or_log2l(v))
+
+
+def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27):
+    devs = np.ascontiguousarray(devs, dtype=np.uint32)
+    hist = np.zeros((len(devs) * ncont, nslots), dtype=np.uint32)
+    dev = np.ascontiguousarray(dev, dtype=np.uint32)
+    cont = np.ascontiguousarray(cont, dtype=np.uint32)
+    delta = np.ascontiguousarray(delta).view(np.int64)
+    lib().or_hist_log2(_p(dev), _p(cont), _p(delta), len(dev), _p(devs), len(devs), ncont,
+                       divisor, nslots, _p(hist))
+    return hist
+
+
+def get_report(slots):
+    """getReport (profile/block-io/tracer/tracer.go:56-90): Data[i] = {Count, 1<<i,
+    (1<<(i+1))-1}, truncated to data[:indexMax] (drops the last non-zero slot)."""
+    data, index_max = [], 0
+    for i, v in enumerate(slots):
+        if v > 0:
+            index_max = i
+        data.append({"count": int(v), "intervalStart": ((1 << (i + 1)) >> 1),
+                     "intervalEnd": (1 << (i + 1)) - 1})
+    return data[:index_max]
+
+
+# ------------------------------------------------------------------------------------
+# synthetic generators (bit-identical with csrc/k_gen.hip)
+# ------------------------------------------------------------------------------------
+def zipf_cdf(G: int, s: float) -> np.ndarray:
+    """u63 fixed-point CDF thresholds of Zipf(s) over ranks 1..G; last == 1<<63."""
+    k = np.arange(1, G + 1, dtype=np.float64)
+    w = k ** (-s)
+    c = np.cumsum(w)
+    c /= c[-1]
+    t = np.minimum(np.floor(c * float(1 << 63)), float(1 << 63)).astype(np.float64)
+    out = np.empty(G, dtype=np.uint64)
+    out[:] = t.astype(np.uint64)
+    out[-1] = np.uint64(1 << 63)
+    return out
+
+
+def lognormal_quantiles(mu: float, sigma: float, nq: int = 4096, cap: int = 1 << 40):
+    """nq+1 monotone quantile boundaries (u64 ns) of lognormal(mu, sigma), capped."""
+    from scipy.stats import norm
+    p = (np.arange(nq + 1, dtype=np.float64) + 0.5) / (nq + 1)
+    q = np.exp(mu + sigma * norm.ppf(p))
+    q = np.minimum(q, float(cap))
+    q = np.maximum.accumulate(np.floor(q)).astype(np.uint64)
+    return q
+
+
+def perm_params(G: int):
+    """Affine bijection r -> (r*A + B) mod G used to scramble key ranks."""
+    A = 999983
+    while math.gcd(A, G) != 1:
+        A += 2
+    return A % G if G > 1 else 1, 12345 % G if G > 1 else 0
+
+
+def gen_tcp(seed, rank, G, cdf, base, n):
+    A, B = perm_params(G)
+    o = {
+        "saddr": np.empty((n, 16), np.uint8), "daddr": np.empty((n, 16), np.uint8),
+        "mntns": np.empty(n, np.uint64), "pid": np.empty(n, np.uint32),
+        "comm": np.empty((n, 16), np.uint8), "lport": np.empty(n, np.uint16),
+        "dport": np.empty(n, np.uint16), "family": np.empty(n, np.uint16),
+        "size": np.empty(n, np.uint32), "dir": np.empty(n, np.uint8),
+    }
+    lib().or_gen_tcp(seed, rank, G, A, B, _p(cdf), base, n,
+                     *[_p(o[k]) for k in ("saddr", "daddr", "mntns", "pid", "comm", "lport",
+                                          "dport", "family", "size", "dir")])
+    return o
+
+
+def gen_open(seed, comm_cdf, base, n):
+    o = {"pid": np.empty(n, np.uint32), "uid": np.empty(n, np.uint32),
+         "mntns": np.empty(n, np.uint64), "comm": np.empty((n, 16), np.uint8),
+         "ret": np.empty(n, np.int64), "fd": np.empty(n, np.int64),
+         "err": np.empty(n, np.int64), "path": np.empty(n, np.uint32)}
+    lib().or_gen_open(seed, _p(comm_cdf), base, n,
+                      *[_p(o[k]) for k in ("pid", "uid", "mntns", "comm", "ret", "fd", "err",
+                                           "path")])
+    return o
+
+
+def gen_bio(seed, q, base, n):
+    o = {"dev": np.empty(n, np.uint32), "cont": np.empty(n, np.uint32),
+         "delta": np.empty(n, np.uint64)}
+    lib().or_gen_bio(seed, _p(q), len(q) - 1, base, n, _p(o["dev"]), _p(o["cont"]),
+                     _p(o["delta"]))
+    return o
+
+
+def gen_np(seed, nsrc, npeer, base, n):
+    o = {"src": np.empty(n, np.uint32), "peer": np.empty(n, np.uint32),
+         "port": np.empty(n, np.uint16), "pkt": np.empty(n, np.uint8),
+         "type": np.empty(n, np.uint8), "proto": np.empty(n, np.uint8),
+         "hostip": np.empty(n, np.uint32), "raddr": np.empty(n, np.uint32)}
+    lib().or_gen_np(seed, nsrc, npeer, base, n,
+                    *[_p(o[k]) for k in ("src", "peer", "port", "pkt", "type", "proto",
+                                         "hostip", "raddr")])
+    return o
+
+
+def gen_file(seed, rank, G, cdf, base, n):
+    A, B = perm_params(G)
+    o = {"inode": np.empty(n, np.uint64), "dev": np.empty(n, np.uint32),
+         "pid": np.empty(n, np.uint32), "tid": np.empty(n, np.uint32),
+         "op": np.empty(n, np.uint8), "count": np.empty(n, np.uint32)}
+    lib().or_gen_file(seed, rank, G, A, B, _p(cdf), base, n,
+                      *[_p(o[k]) for k in ("inode", "dev", "pid", "tid", "op", "count")])
+    return o
+
+
+TCP_KEY_COLS = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family")
+
+
+def pack_cols(batch, names):
+    """Concatenate SoA columns row-wise into a (n, kb) uint8 key matrix."""
+    parts = []
+    for nm in names:
+        a = np.ascontiguousarray(batch[nm])
+        n = a.shape[0]
+        parts.append(a.view(np.uint8).reshape(n, -1))
+    return np.concatenate(parts, axis=1)
+
+
+def top_tcp(ev, k=20, base_idx=0, max_groups=None):
+    """Reference-shaped CPU path (igx_oracle.c §6).  Returns (G, rows) where rows are
+    dicts for the first k sorted stats."""
+    n = len(ev["pid"])
+    maxG = max_groups or n
+    keys = np.empty((k, 72), np.uint8)
+    sent, recv, first = (np.empty(k, np.uint64) for _ in range(3))
+    cols = [np.ascontiguousarray(ev[c]) for c in ("saddr", "daddr", "mntns", "pid", "comm",
+                                                  "lport", "dport", "family", "size", "dir")]
+    G = lib().or_top_tcp(*[_p(c) for c in cols], n, base_idx, maxG, k, _p(keys), _p(sent),
+                         _p(recv), _p(first))
+    m = min(k, G)
+    return G, keys[:m], sent[:m], recv[:m], first[:m]
+
+
+# ------------------------------------------------------------------------------------
+# GroupEntries (pkg/columns/group/group.go:27-165) on Python row objects
+# ------------------------------------------------------------------------------------
+def _go_string_from_value(v, kind):
+    # getStringFromValue (group.go:27-47)
+    cls = KIND_CLASS[kind][0]
+    if cls in ("int", "uint"):
+        return str(int(v))
+    if cls == "float":
+        return _go_format_float_E(float(v))
+    return str(v)
+
+
+def _go_format_float_E(f):
+    """strconv.FormatFloat(f, 'E', -1, 64): shortest round-trip digits, d.dddE+dd."""
+    if f != f:
+        return "NaN"
+    if math.isinf(f):
+        return "+Inf" if f > 0 else "-Inf"
+    if f == 0:
+        return ("-" if math.copysign(1, f) < 0 else "") + "0E+00"
+    s = repr(abs(f))
+    mant, ex = (s.split("e")[0], int(s.split("e")[1])) if "e" in s else (s, 0)
+    ip, fp = mant.split(".") if "." in mant else (mant, "")
+    digits = ip + fp
+    point = len(ip) + ex
+    stripped = digits.lstrip("0")
+    lead = len(digits) - len(stripped)
+    stripped = stripped.rstrip("0")
+    e10 = point - lead - 1
+    m = stripped[0] + ("." + stripped[1:] if len(stripped) > 1 else "")
+    return ("-" if f < 0 else "") + m + "E" + ("+" if e10 >= 0 else "-") + "%02d" % abs(e10)
+
+
+def group_entries(cols: dict, entries: list, group_by: list, sum_cols: dict):
+    """GroupEntries.  entries: list of dicts (None = nil).  cols: lower-name -> OCol.
+    sum_cols: name -> kind for `group:sum` columns.  Map order is replaced by the
+    canonical first-occurrence order; the result of each pass is then
+    sorted ascending by the group column exactly as group.go:115 does."""
+    if entries is None:
+        return None, None
+    new = entries
+    for gname in group_by:
+        gname = gname.lower()
+        if gname == "":
+            vals = [e for e in entries if e is not None]
+            return [_flatten(vals, sum_cols)] if vals else [], None
+        col = cols.get(gname)
+        if col is None:
+            return None, FilterError(f'could not group by "{gname}": column not found')
+        groups = {}
+        for e in new:
+            if e is None:
+                continue
+            groups.setdefault(_go_string_from_value(e[col.name], col.kind), []).append(e)
+        out = [_flatten(v, sum_cols) for v in groups.values()]
+        out = go_sort_entries_py(out, [(lambda r, n=col.name: r[n], False)])
+        new = out
+    return new, None
+
+
+def _flatten(vals, sum_cols):
+    base = dict(vals[0])
+    for v in vals[1:]:
+        for name, kind in sum_cols.items():
+            cls, w = KIND_CLASS[kind]
+            if cls == "float":
+                base[name] = base[name] + v[name]
+            else:
+                s = int(base[name]) + int(v[name])
+                s &= (1 << (8 * w)) - 1
+                if cls == "int" and s >= 1 << (8 * w - 1):
+                    s -= 1 << (8 * w)
+                base[name] = s
+    return base
