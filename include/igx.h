@@ -1,0 +1,242 @@
+/*
+ * igx.h -- C ABI of the MI355X-native Inspektor Gadget event-aggregation path.
+ *
+ * One shared library, libigx.so (HIP kernels for gfx950 + host C++), built in-tree at
+ * inspektor-gadget_amd/libigx.so.  Plain pointers and sizes only; nothing here knows
+ * about torch or Go types, so the reference's Go packages can bind it with cgo
+ * (INTEGRATION.md shows the binding).
+ *
+ * Reference interfaces replaced (paths relative to the reference repository root):
+ *   igx_filter_parse        filter.GetFilterFromString       pkg/columns/filter/filter.go:91-172
+ *                           (+ getValueFromFilterSpec :53-87)
+ *   igx_filter              filter.FilterEntries / FilterSpecs.MatchAll
+ *                                                             pkg/columns/filter/filter.go:266-325
+ *   igx_sort_prepare        sort.Prepare / FilterSortableColumns / CanSortBy
+ *                                                             pkg/columns/sort/sort.go:87-111,139-178
+ *   igx_sort_perm           ColumnSorterCollection.Sort / SortEntries
+ *                                                             pkg/columns/sort/sort.go:35-83,116-123
+ *   igx_topk                top.SortStats + stats[:MaxRows]  pkg/gadgets/top/top.go:39-41,
+ *                                                             pkg/gadgets/top/tcp/tracer/tracer.go:249-253
+ *   igx_groupby_*           BPF hash-map keyed aggregation + nextStats drain
+ *                                                             pkg/gadgets/top/tcp/tracer/bpf/tcptop.bpf.c:33-110,
+ *                                                             pkg/gadgets/top/tcp/tracer/tracer.go:147-226,
+ *                                                             pkg/gadgets/top/file/tracer/bpf/filetop.bpf.c:39-94,
+ *                                                             pkg/gadgets/top/block-io/tracer/bpf/biotop.bpf.c:85-130,
+ *                                                             pkg/gadgets/trace/network/tracer/bpf/graph.c:102-114
+ *                           and group.GroupEntries (one column per call)
+ *                                                             pkg/columns/group/group.go:51-121
+ *   igx_hist_log2           biolatency histogram              pkg/gadgets/profile/block-io/tracer/bpf/biolatency.bpf.c:100-154
+ *                                                             pkg/gadgets/profile/block-io/tracer/bpf/bits.bpf.h:8-29
+ *
+ * Conventions
+ *   - Return codes: IGX_OK (0) or a negative errno-style code.  The message of the last
+ *     failure on a context is igx_last_error(ctx); host-only parsers write theirs into
+ *     a caller buffer (the Go `error` text, e.g. `could not apply filter: column "x" not
+ *     found`).
+ *   - "device" pointers are HIP device allocations (igx_malloc or any HIP allocator);
+ *     "host" pointers are plain memory.  Nothing is retained past the call except by
+ *     igx_table objects, which own their device storage (cgo pointer rules).
+ *   - Every device operation is enqueued on the context's stream (igx_set_stream to share
+ *     a caller's stream) and is asynchronous unless documented as synchronising.
+ */
+#ifndef IGX_H
+#define IGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IGX_OK 0
+#define IGX_ENOENT (-2)
+#define IGX_EIO (-5)
+#define IGX_ENOMEM (-12)
+#define IGX_EINVAL (-22)
+#define IGX_ENOSPC (-28)
+#define IGX_ENOTSUP (-95)
+
+/* Column kind classes (Go reflect kinds collapsed by arithmetic).  Strings are fixed-width
+ * zero-padded byte columns: bytewise unsigned compare == Go string compare because
+ * gadgets.FromCString never yields NUL (pkg/gadgets/helpers.go:76-83). */
+enum igx_kind {
+    IGX_KIND_INT = 0,   /* int, int8..int64 (two's complement, little-endian) */
+    IGX_KIND_UINT = 1,  /* uint, uint8..uint64 */
+    IGX_KIND_FLOAT = 2, /* float32 / float64 */
+    IGX_KIND_BYTES = 3, /* string as fixed-width bytes */
+    IGX_KIND_BOOL = 4,  /* bool: not filterable (filter.go:54-85), not sortable (sort.go:77-78) */
+    IGX_KIND_OTHER = 5  /* struct and everything else */
+};
+
+enum igx_cmp { IGX_CMP_EQ = 0, IGX_CMP_REGEX = 1, IGX_CMP_LT = 2, IGX_CMP_LE = 3,
+               IGX_CMP_GT = 4, IGX_CMP_GE = 5 };
+
+#define IGX_COL_VIRTUAL 1u   /* columns.AddColumn virtual column (columns.go:282-309) */
+#define IGX_COL_EXTRACTOR 2u /* column with SetExtractor (columns.go:320-332) */
+#define IGX_NO_COL 0xFFFFFFFFu
+#define IGX_MAX_REF 256
+#define IGX_MAX_KEY_BYTES 128
+
+/* Schema entry: one column of the event struct T, as derived by columns.NewColumns. */
+typedef struct {
+    const char *name; /* column name; matched case-insensitively (columns.go:83-86) */
+    uint32_t kind;    /* enum igx_kind */
+    uint32_t width;   /* bytes per row in the SoA batch */
+    uint32_t flags;   /* IGX_COL_* */
+    uint32_t raw_kind;/* kind used for sorting extractor columns (sort.go:46-48) */
+} igx_schema_col;
+
+/* Device column: row i lives at ptr + i*width. */
+typedef struct {
+    const void *ptr;
+    uint32_t width;
+    uint32_t kind;
+} igx_col;
+
+/* One compiled filter (FilterSpec).  ref holds the reference value already converted to
+ * the column type (reflect Convert truncation, filter.go:64,74). */
+typedef struct {
+    uint32_t col;     /* index into the schema / column array */
+    uint32_t cmp;     /* enum igx_cmp */
+    uint32_t negate;
+    uint32_t ref_len; /* valid bytes in ref */
+    uint8_t ref[IGX_MAX_REF];
+} igx_pred;
+
+/* One sort key as Prepare emits it, in sortBy order (first = highest priority). */
+typedef struct {
+    const void *ptr;  /* device column (igx_sort_perm) or unused (igx_sort_prepare) */
+    uint32_t width;
+    uint32_t kind;
+    uint32_t desc;    /* 1 when the sortBy entry had the '-' prefix */
+    uint32_t col;     /* schema index (igx_sort_prepare output) */
+} igx_sortkey;
+
+typedef struct igx_ctx igx_ctx;
+typedef struct igx_table igx_table;
+
+/* ---- context ------------------------------------------------------------------------ */
+int igx_open(int device, uint32_t flags, igx_ctx **out);
+int igx_close(igx_ctx *ctx);
+const char *igx_last_error(igx_ctx *ctx);
+/* Share a caller's hipStream_t (NULL = HIP's default/null stream, which is what torch's
+ * default stream is).  Until the first call the context uses a stream of its own. */
+int igx_set_stream(igx_ctx *ctx, void *hip_stream);
+void *igx_get_stream(igx_ctx *ctx);
+int igx_sync(igx_ctx *ctx);
+int igx_malloc(igx_ctx *ctx, size_t bytes, void **out);
+int igx_free(igx_ctx *ctx, void *p);
+int igx_memcpy_h2d(igx_ctx *ctx, void *dst, const void *src, size_t bytes);   /* sync */
+int igx_memcpy_d2h(igx_ctx *ctx, void *dst, const void *src, size_t bytes);   /* sync */
+int igx_memcpy_d2d(igx_ctx *ctx, void *dst, const void *src, size_t bytes);   /* async */
+int igx_version(void);
+
+/* ---- filter (host parser + device scan) -------------------------------------------- */
+/* GetFilterFromString: parses "col[:[!][~|>=|>|<=|<]value]".  Host only, no GPU needed.
+ * Regex rules parse (and are returned with cmp=IGX_CMP_REGEX) but the device scan rejects
+ * them with IGX_ENOTSUP.  errbuf receives the Go error text. */
+int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *filter,
+                     igx_pred *out, char *errbuf, size_t errlen);
+
+/* FilterEntries / MatchAll: AND of preds over rows [0,nrows), order-preserving.
+ * valid (device, nullable): 0 marks a nil entry (skipped).  out_idx (device) receives
+ * the selected row ids; *out_n (device u64) their count.  Asynchronous. */
+int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+               uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+               uint64_t *out_n);
+
+/* ---- sort / top-K -------------------------------------------------------------------- */
+/* Prepare + FilterSortableColumns: keeps valid keys in sortBy order (unknown, empty and
+ * virtual columns dropped).  *out_n = number of valid keys; *out_invalid = dropped ones.
+ * Bool / unsupported kinds stay in the list (the Go code skips them at Sort time,
+ * sort.go:77-78) and are skipped by igx_sort_perm.  Host only. */
+int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, const char *const *sort_by,
+                     uint32_t n, igx_sortkey *out, uint32_t *out_n, uint32_t *out_invalid);
+
+/* Sort permutation with the exact tie order of Go 1.19 sort.SliceStable under
+ * getLessFunc (SURVEY.md §0.3 closed form).  pos (device u64, nullable): pre-sort position
+ * of each row (NULL = row index).  valid (device, nullable): nil rows sort last.
+ * out_perm (device u32, nrows).  Asynchronous. */
+int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
+                  const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm);
+
+/* First k rows of the igx_sort_perm order (SortStats + truncate to max-rows).
+ * out_idx (device u32, k).  Asynchronous. */
+int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
+             const uint64_t *pos, uint32_t k, uint32_t *out_idx);
+
+/* ---- keyed aggregation (group-by) ------------------------------------------------------ */
+enum igx_agg_kind { IGX_AGG_COUNT = 0, IGX_AGG_SUM = 1 };
+
+typedef struct {
+    uint32_t kind;      /* enum igx_agg_kind */
+    uint32_t col;       /* value column index (SUM) */
+    uint32_t cond_col;  /* IGX_NO_COL or column whose value must equal cond_val */
+    uint32_t out_width; /* result wraps to this many bytes (1,2,4,8) */
+    uint64_t cond_val;
+} igx_agg;
+
+typedef struct {
+    uint64_t n_groups;        /* host copy, valid after igx_groupby_finalize */
+    uint32_t key_bytes;       /* packed key bytes per group (each key column padded to 4) */
+    uint32_t key_stride;      /* bytes between consecutive keys in `keys` */
+    uint32_t naggs;
+    const uint8_t *keys;      /* device: n_groups x key_stride */
+    const uint64_t *aggs[16]; /* device: one u64 array per aggregate, indexed by group */
+    const uint64_t *first_idx;/* device: first-occurrence event index per group */
+    const uint64_t *d_n_groups;/* device: group count */
+} igx_table_view;
+
+/* capacity = maximum number of distinct groups.  key_widths: byte width of each key
+ * column (packed, each padded to a multiple of 4). */
+int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys,
+                       const igx_agg *aggs, uint32_t naggs, uint64_t capacity,
+                       igx_table **out);
+/* Aggregate rows [0,nrows) of cols into the table; key_cols selects the key columns
+ * (in the table's key order); preds are AND-ed filters applied first (the BPF probe
+ * checks).  base_idx is the global index of row 0 (first-occurrence order).  Async. */
+int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols,
+                       const uint32_t *key_cols, const igx_pred *preds, uint32_t npreds,
+                       uint64_t nrows, uint64_t base_idx);
+/* Synchronises; fills the view; IGX_ENOSPC if capacity was exceeded. */
+int igx_groupby_finalize(igx_table *t, igx_table_view *view);
+/* Materialise groups idx[0..k) (device u32, e.g. igx_topk output) as packed rows of
+ * key_bytes | naggs x u64 | first_idx u64 into out_rows (device) -- the Stats rows
+ * nextStats builds (pkg/gadgets/top/tcp/tracer/tracer.go:186-219).  Call after
+ * igx_groupby_finalize.  Asynchronous. */
+int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows);
+int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete loop) */
+int igx_groupby_destroy(igx_table *t);
+
+/* ---- log2 latency histograms ---------------------------------------------------------- */
+/* hist[(dev_index(dev)*ncont + cont) * nslots + slot] += 1 for every row with delta >= 0
+ * (delta is s64 ns), slot = min(log2l(delta/divisor), nslots-1).  devs (host, ndev <= 64)
+ * lists the device numbers (dev_index = position); rows with other devs are ignored.
+ * cont may be NULL (ncont must then be 1).  hist (device u32) accumulates.  Async. */
+int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
+                  const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
+                  uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
+
+/* ---- synthetic event generators (device; bit-identical with oracle/igx_oracle.c) ---- */
+int igx_gen_tcp(igx_ctx *ctx, uint64_t seed, uint64_t rank, uint64_t G, uint64_t permA,
+                uint64_t permB, const uint64_t *cdf, uint64_t base, uint64_t n, uint8_t *saddr,
+                uint8_t *daddr, uint64_t *mntns, uint32_t *pid, uint8_t *comm, uint16_t *lport,
+                uint16_t *dport, uint16_t *family, uint32_t *size, uint8_t *dir);
+int igx_gen_open(igx_ctx *ctx, uint64_t seed, const uint64_t *comm_cdf, uint64_t base,
+                 uint64_t n, uint32_t *pid, uint32_t *uid, uint64_t *mntns, uint8_t *comm,
+                 int64_t *ret, int64_t *fd, int64_t *err, uint32_t *path_id);
+int igx_gen_bio(igx_ctx *ctx, uint64_t seed, const uint64_t *q, uint64_t nq, uint64_t base,
+                uint64_t n, uint32_t *dev, uint32_t *cont, uint64_t *delta);
+int igx_gen_np(igx_ctx *ctx, uint64_t seed, uint64_t nsrc, uint64_t npeer, uint64_t base,
+               uint64_t n, uint32_t *src, uint32_t *peer, uint16_t *port, uint8_t *pkt,
+               uint8_t *typ, uint8_t *proto, uint32_t *hostip, uint32_t *raddr);
+int igx_gen_file(igx_ctx *ctx, uint64_t seed, uint64_t rank, uint64_t G, uint64_t permA,
+                 uint64_t permB, const uint64_t *cdf, uint64_t base, uint64_t n,
+                 uint64_t *inode, uint32_t *dev, uint32_t *pid, uint32_t *tid, uint8_t *op,
+                 uint32_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IGX_H */

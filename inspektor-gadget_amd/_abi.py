@@ -1,0 +1,119 @@
+"""ctypes mirror of include/igx.h (the C ABI of libigx.so).
+
+This is the same surface a Go caller binds with cgo; the Python host
+layer uses it so the parity tests exercise exactly what a drop-in caller would call.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libigx.so")
+
+IGX_OK = 0
+IGX_ENOENT = -2
+IGX_EIO = -5
+IGX_ENOMEM = -12
+IGX_EINVAL = -22
+IGX_ENOSPC = -28
+IGX_ENOTSUP = -95
+
+KIND_INT, KIND_UINT, KIND_FLOAT, KIND_BYTES, KIND_BOOL, KIND_OTHER = range(6)
+CMP_EQ, CMP_REGEX, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
+COL_VIRTUAL, COL_EXTRACTOR = 1, 2
+NO_COL = 0xFFFFFFFF
+MAX_REF = 256
+AGG_COUNT, AGG_SUM = 0, 1
+
+
+class SchemaCol(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("kind", C.c_uint32), ("width", C.c_uint32),
+                ("flags", C.c_uint32), ("raw_kind", C.c_uint32)]
+
+
+class Col(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("kind", C.c_uint32)]
+
+
+class Pred(C.Structure):
+    _fields_ = [("col", C.c_uint32), ("cmp", C.c_uint32), ("negate", C.c_uint32),
+                ("ref_len", C.c_uint32), ("ref", C.c_uint8 * MAX_REF)]
+
+
+class SortKey(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("kind", C.c_uint32),
+                ("desc", C.c_uint32), ("col", C.c_uint32)]
+
+
+class Agg(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("col", C.c_uint32), ("cond_col", C.c_uint32),
+                ("out_width", C.c_uint32), ("cond_val", C.c_uint64)]
+
+
+class TableView(C.Structure):
+    _fields_ = [("n_groups", C.c_uint64), ("key_bytes", C.c_uint32), ("key_stride", C.c_uint32),
+                ("naggs", C.c_uint32), ("keys", C.c_void_p), ("aggs", C.c_void_p * 16),
+                ("first_idx", C.c_void_p), ("d_n_groups", C.c_void_p)]
+
+
+class IgxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"igx error {code}: {msg}")
+        self.code = code
+
+
+# (name, restype, argtypes) for every symbol of include/igx.h
+_VP, _U32, _U64, _SZ, _I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
+SIGNATURES = [
+    ("igx_open", _I, [_I, _U32, C.POINTER(_VP)]),
+    ("igx_close", _I, [_VP]),
+    ("igx_last_error", C.c_char_p, [_VP]),
+    ("igx_set_stream", _I, [_VP, _VP]),
+    ("igx_get_stream", _VP, [_VP]),
+    ("igx_sync", _I, [_VP]),
+    ("igx_malloc", _I, [_VP, _SZ, C.POINTER(_VP)]),
+    ("igx_free", _I, [_VP, _VP]),
+    ("igx_memcpy_h2d", _I, [_VP, _VP, _VP, _SZ]),
+    ("igx_memcpy_d2h", _I, [_VP, _VP, _VP, _SZ]),
+    ("igx_memcpy_d2d", _I, [_VP, _VP, _VP, _SZ]),
+    ("igx_version", _I, []),
+    ("igx_filter_parse", _I, [C.POINTER(SchemaCol), _U32, C.c_char_p, C.POINTER(Pred),
+                              C.c_char_p, _SZ]),
+    ("igx_filter", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _VP, _VP]),
+    ("igx_sort_prepare", _I, [C.POINTER(SchemaCol), _U32, C.POINTER(C.c_char_p), _U32,
+                              C.POINTER(SortKey), C.POINTER(_U32), C.POINTER(_U32)]),
+    ("igx_sort_perm", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP]),
+    ("igx_topk", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _U32, _VP]),
+    ("igx_groupby_create", _I, [_VP, C.POINTER(_U32), _U32, C.POINTER(Agg), _U32, _U64,
+                                C.POINTER(_VP)]),
+    ("igx_groupby_update", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(_U32), C.POINTER(Pred),
+                                _U32, _U64, _U64]),
+    ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
+    ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
+    ("igx_groupby_reset", _I, [_VP]),
+    ("igx_groupby_destroy", _I, [_VP]),
+    ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
+                           _VP]),
+    ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),
+    ("igx_gen_open", _I, [_VP, _U64, _VP, _U64, _U64] + [_VP] * 8),
+    ("igx_gen_bio", _I, [_VP, _U64, _VP, _U64, _U64, _U64, _VP, _VP, _VP]),
+    ("igx_gen_np", _I, [_VP, _U64, _U64, _U64, _U64, _U64] + [_VP] * 8),
+    ("igx_gen_file", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 6),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libigx.so.  There is no fallback: the product path fails loudly without it."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                              "(or `make -C inspektor-gadget_amd/csrc`)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib

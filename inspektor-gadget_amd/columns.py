@@ -1,0 +1,223 @@
+"""Column schema + SoA event batches (the pkg/columns analogue).
+
+Reference: pkg/columns/columns.go (NewColumns :51, GetColumn lower-cases :83-86,
+AddColumn virtual columns :282-309, SetExtractor :320-332) and columninfo.go (Column
+:43-66, `group:sum` tag :159-171).  The reference reads fields of []*T through reflection
+offsets (GetField, columns.go:343-347); here every column is a device array (SoA) of a
+fixed width, which is what the gfx950 kernels stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from . import _abi
+from .runtime import torch_mod
+
+# Go reflect kind -> (igx kind class, width in bytes; strings take their declared width)
+KINDS = {
+    "int": (_abi.KIND_INT, 8), "int8": (_abi.KIND_INT, 1), "int16": (_abi.KIND_INT, 2),
+    "int32": (_abi.KIND_INT, 4), "int64": (_abi.KIND_INT, 8),
+    "uint": (_abi.KIND_UINT, 8), "uint8": (_abi.KIND_UINT, 1), "uint16": (_abi.KIND_UINT, 2),
+    "uint32": (_abi.KIND_UINT, 4), "uint64": (_abi.KIND_UINT, 8),
+    "float32": (_abi.KIND_FLOAT, 4), "float64": (_abi.KIND_FLOAT, 8),
+    "string": (_abi.KIND_BYTES, None), "bool": (_abi.KIND_BOOL, 1),
+    "struct": (_abi.KIND_OTHER, 0),
+}
+
+GroupTypeNone, GroupTypeSum = 0, 1          # types.go:26-31
+OrderAsc, OrderDesc = True, False           # types.go:37-38
+
+
+def torch_dtype(kind: str):
+    torch = torch_mod()
+    return {"int": torch.int64, "int8": torch.int8, "int16": torch.int16, "int32": torch.int32,
+            "int64": torch.int64, "uint": torch.uint64, "uint8": torch.uint8,
+            "uint16": torch.uint16, "uint32": torch.uint32, "uint64": torch.uint64,
+            "float32": torch.float32, "float64": torch.float64, "bool": torch.bool}[kind]
+
+
+@dataclass
+class Column:
+    Name: str
+    kind: str                        # Go reflect kind name
+    width: int = 0                   # bytes per row (strings: fixed width)
+    GroupType: int = GroupTypeNone
+    virtual: bool = False
+    extractor: Optional[Callable] = None
+
+    def Kind(self):
+        return self.kind
+
+    def IsVirtual(self):
+        return self.virtual
+
+    def HasCustomExtractor(self):
+        return self.extractor is not None
+
+    @property
+    def igx_kind(self):
+        return KINDS[self.kind][0]
+
+
+class Columns:
+    """NewColumns[T] for a flat SoA schema.  fields: (name, kind[, width][, "group:sum"])."""
+
+    def __init__(self, fields=()):
+        self._cols: Dict[str, Column] = {}
+        self._order: List[str] = []
+        for f in fields:
+            name, kind = f[0], f[1]
+            width = None
+            group = GroupTypeNone
+            for extra in f[2:]:
+                if isinstance(extra, int):
+                    width = extra
+                elif extra == "group:sum":
+                    group = GroupTypeSum
+            kc, w = KINDS[kind]
+            if w is None:
+                if width is None:
+                    raise ValueError(f"string column {name!r} needs a fixed width")
+                w = width
+            self._add(Column(name, kind, w, group))
+
+    def _add(self, col: Column):
+        key = col.Name.lower()
+        if key in self._cols:
+            raise ValueError(f"duplicate column name {col.Name!r}")
+        self._cols[key] = col
+        self._order.append(key)
+        self._schema = None
+
+    # -- reference API -------------------------------------------------------------
+    def GetColumn(self, name: str):
+        c = self._cols.get(name.lower())
+        return c, c is not None
+
+    def GetColumnMap(self):
+        return self
+
+    def GetOrderedColumns(self):
+        return [self._cols[k] for k in self._order]
+
+    def AddColumn(self, name: str, extractor: Callable):
+        """Virtual column (columns.go:282-309): kind String, no backing field."""
+        self._add(Column(name, "string", 0, virtual=True, extractor=extractor))
+
+    def SetExtractor(self, name: str, fn: Callable):
+        """columns.go:320-332; sorting still uses the raw field kind (sort.go:46-48)."""
+        c, ok = self.GetColumn(name)
+        if not ok:
+            raise KeyError(name)
+        c.extractor = fn
+        self._schema = None
+
+    MustAddColumn = AddColumn
+    MustSetExtractor = SetExtractor
+
+    # -- igx plumbing ----------------------------------------------------------------
+    def index(self, name: str) -> int:
+        return self._order.index(name.lower())
+
+    def names(self):
+        return [self._cols[k].Name for k in self._order]
+
+    def schema(self):
+        """ctypes igx_schema_col array (cached; names kept alive on self)."""
+        if self._schema is None:
+            cols = self.GetOrderedColumns()
+            self._names = [c.Name.lower().encode() for c in cols]
+            arr = (_abi.SchemaCol * max(1, len(cols)))()
+            for i, c in enumerate(cols):
+                flags = (_abi.COL_VIRTUAL if c.virtual else 0) | \
+                        (_abi.COL_EXTRACTOR if (c.extractor and not c.virtual) else 0)
+                kind = _abi.KIND_BYTES if (c.extractor is not None) else c.igx_kind
+                arr[i] = _abi.SchemaCol(self._names[i], kind, c.width, flags, c.igx_kind)
+            self._schema = (arr, len(cols))
+        return self._schema
+
+
+class EventBatch:
+    """SoA batch on the device: name -> tensor ((n,) scalars or (n, W) uint8 strings),
+    plus an optional `valid` uint8 mask (0 = nil entry, as a nil *T in the reference)."""
+
+    def __init__(self, cols: Columns, data: dict, valid=None):
+        self.cols = cols
+        self.data = {k.lower(): v for k, v in data.items()}
+        self.valid = valid
+        any_t = next(iter(self.data.values())) if self.data else valid
+        self.n = 0 if any_t is None else int(any_t.shape[0])
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, name):
+        return self.data[name.lower()]
+
+    def device(self):
+        t = next(iter(self.data.values()))
+        return t.device
+
+    def tensors_in_schema_order(self):
+        """One tensor per schema column (virtual columns get a 1-byte placeholder)."""
+        torch = torch_mod()
+        out = []
+        for c in self.cols.GetOrderedColumns():
+            t = self.data.get(c.Name.lower())
+            if t is None:
+                t = torch.zeros(max(1, self.n), dtype=torch.uint8, device=self.device())
+            out.append(t)
+        return out
+
+    def take(self, idx):
+        """Gather rows (device), keeping column dtypes."""
+        torch = torch_mod()
+        li = idx.to(torch.int64)
+        out = {k: gather(v, li) for k, v in self.data.items()}
+        valid = None if self.valid is None else self.valid.index_select(0, li)
+        return EventBatch(self.cols, out, valid)
+
+    def to_host(self):
+        return {k: host(v) for k, v in self.data.items()}
+
+
+_VIEW_AS = None
+
+
+def gather(t, li):
+    """index_select for every dtype (unsigned shell dtypes gather through a signed view)."""
+    torch = torch_mod()
+    global _VIEW_AS
+    if _VIEW_AS is None:
+        _VIEW_AS = {torch.uint16: torch.int16, torch.uint32: torch.int32, torch.uint64: torch.int64}
+    alt = _VIEW_AS.get(t.dtype)
+    if alt is not None:
+        return t.view(alt).index_select(0, li).view(t.dtype)
+    return t.index_select(0, li)
+
+
+def host(t):
+    """Device tensor -> numpy (unsigned shell dtypes through a signed view)."""
+    import numpy as np
+    torch = torch_mod()
+    m = {torch.uint16: (torch.int16, np.uint16), torch.uint32: (torch.int32, np.uint32),
+         torch.uint64: (torch.int64, np.uint64)}
+    if t.dtype in m:
+        alt, npd = m[t.dtype]
+        return t.view(alt).cpu().numpy().view(npd)
+    return t.cpu().numpy()
+
+
+def to_device(a, device="cuda"):
+    """numpy -> device tensor keeping unsigned widths."""
+    import numpy as np
+    torch = torch_mod()
+    m = {np.dtype(np.uint16): (np.int16, torch.uint16), np.dtype(np.uint32): (np.int32, torch.uint32),
+         np.dtype(np.uint64): (np.int64, torch.uint64)}
+    a = np.ascontiguousarray(a)
+    if a.dtype in m:
+        sd, td = m[a.dtype]
+        return torch.from_numpy(a.view(sd)).to(device).view(td)
+    return torch.from_numpy(a).to(device)

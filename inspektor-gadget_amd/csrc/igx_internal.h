@@ -1,0 +1,77 @@
+// igx_internal.h -- shared host/device declarations for libigx.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/igx.h"
+
+#define IGX_VERSION 1
+
+struct igx_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // grow-only scratch arena (kernels never hipMalloc inside a call once warmed up)
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // pinned host staging for small readbacks
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
+};
+
+// sets ctx->err and returns code
+int igx_fail(igx_ctx *ctx, int code, const char *fmt, ...);
+// hipError_t -> IGX_EIO with message
+#define IGX_HIP(ctx, expr)                                                            \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return igx_fail((ctx), IGX_EIO, "%s: %s", #expr, hipGetErrorString(e_));  \
+    } while (0)
+
+// scratch: returns a device pointer with at least `bytes` (16-B aligned sub-buffers are
+// carved by the caller).  May synchronise the stream when it has to grow.
+int igx_scratch(igx_ctx *ctx, size_t bytes, void **out);
+int igx_pinned(igx_ctx *ctx, size_t bytes, void **out);
+
+static inline size_t igx_align(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------------
+// device-side predicate (compiled igx_pred + column), passed by value in kernargs
+// ---------------------------------------------------------------------------------
+#define IGX_KMAX_PREDS 4
+struct DevPred {
+    const uint8_t *ptr;
+    uint32_t width, kind, cmp, negate;
+    uint32_t ref_len, pad;
+    uint8_t ref[IGX_MAX_REF];
+};
+struct DevPreds {
+    uint32_t n, pad;
+    DevPred p[IGX_KMAX_PREDS];
+};
+int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                    uint32_t npreds, DevPreds *out);
+
+// ---------------------------------------------------------------------------------
+// launchers (defined in the k_*.hip files)
+// ---------------------------------------------------------------------------------
+int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64_t nrows,
+                  uint32_t *out_idx, uint64_t *out_n);
+
+struct SortPlanKey {
+    const uint8_t *ptr;
+    uint32_t width, kind, desc_eff, words;
+};
+int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
+                     const uint64_t *pos, bool pos_not, const uint8_t *valid,
+                     uint32_t *out_perm, uint32_t limit);
+
+int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
+                     const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
+                     uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);

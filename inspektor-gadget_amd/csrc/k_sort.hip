@@ -1,0 +1,333 @@
+// k_sort.hip -- stable LSD radix sort reproducing the reference's tie order (kernel (3)).
+//
+// Reference: ColumnSorterCollection.Sort (pkg/columns/sort/sort.go:35-83) runs one Go
+// 1.19 sort.SliceStable pass per key, last key first, with getLessFunc (:125-135)
+// `!(a<b) != order`.  For DESC that comparator is `a >= b`; SliceStable always asks
+// less(later, earlier), so every DESC pass reverses ties.  The composite order is
+// therefore a single lexicographic order (verified by
+// tests/test_oracle_golden.py::test_closed_form_matches_go_stable):
+//   key i compares in direction desc_i XOR desc_1 ^ ... ^ desc_{i-1}, and the final
+//   tie-break is the pre-sort position, ascending iff sum(desc) is even.
+// nil entries (valid==0) sort last (sort.go:127-132), in input order.
+//
+// Implementation: compose every row into big-endian u32 words (SoA, most significant
+// word first), one word group per key; DESC keys are bit-NOT-ed, signed ints get their
+// sign bit flipped, floats the IEEE total-order flip, strings stay big-endian bytes; the
+// position goes last (NOT-ed when the parity is odd).  One AND/OR reduction finds the
+// byte digits that are constant over all rows; only the others get a pass.  Each pass is
+// histogram -> scan -> stable scatter (wave64 ballot multi-split ranks, tile order kept
+// by per-digit running counters in LDS).  Words below the current digit are no longer
+// carried (LSD never reads them again).
+#include <vector>
+
+#include "k_common.h"
+
+namespace {
+
+constexpr int TB = 256;
+constexpr int IPT = 16;
+constexpr int TILE = TB * IPT;   // 4096 rows per tile
+constexpr int MAXW = 80;          // composed words (<= 8 keys x 64-byte strings + pos + nil)
+
+struct ComposeArgs {
+    const uint8_t *ptr[8];
+    uint32_t width[8], kind[8], desc[8], words[8];
+    uint32_t nkeys, has_nil, pos_words, pos_not;
+    const uint64_t *pos;
+    const uint8_t *valid;
+    uint64_t n, stride;   // stride = words array pitch (elements)
+};
+
+__device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, uint32_t j) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t o = 4 * j + b;
+        v = (v << 8) | (o < width ? p[o] : 0u);
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
+                                                uint32_t *__restrict__ payload) {
+    uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= a.n) return;
+    bool nil = a.valid && a.valid[i] == 0;
+    uint32_t w = 0;
+    if (a.has_nil) words[(w++) * a.stride + i] = nil ? 1u : 0u;
+    for (uint32_t k = 0; k < a.nkeys; ++k) {
+        const uint32_t nw = a.words[k];
+        if (nil) {
+            for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = 0;
+            w += nw;
+            continue;
+        }
+        const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
+        if (a.kind[k] == IGX_KIND_BYTES) {
+            const uint8_t *p = a.ptr[k] + i * a.width[k];
+            for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
+        } else if (a.kind[k] == IGX_KIND_FLOAT) {
+            if (a.width[k] == 4) {
+                uint32_t b = reinterpret_cast<const uint32_t *>(a.ptr[k])[i];
+                if (b == 0x80000000u) b = 0;                       // -0 == +0 in Go
+                b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+                words[w * a.stride + i] = b ^ inv;
+            } else {
+                uint64_t b = reinterpret_cast<const uint64_t *>(a.ptr[k])[i];
+                if (b == 0x8000000000000000ull) b = 0;
+                b = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+                words[w * a.stride + i] = (uint32_t)(b >> 32) ^ inv;
+                words[(w + 1) * a.stride + i] = (uint32_t)b ^ inv;
+            }
+        } else {
+            const bool sgn = a.kind[k] == IGX_KIND_INT;
+            uint64_t v = ld_scalar(a.ptr[k], a.width[k], i, false);
+            if (sgn) v ^= 1ull << (8 * a.width[k] - 1);
+            if (nw == 1) {
+                words[w * a.stride + i] = (uint32_t)v ^ inv;
+            } else {
+                words[w * a.stride + i] = (uint32_t)(v >> 32) ^ inv;
+                words[(w + 1) * a.stride + i] = (uint32_t)v ^ inv;
+            }
+        }
+        w += nw;
+    }
+    uint64_t p = a.pos ? a.pos[i] : i;
+    if (a.pos_not && !nil) p = ~p;
+    if (a.pos_words == 2) {
+        words[w * a.stride + i] = (uint32_t)(p >> 32);
+        words[(w + 1) * a.stride + i] = (uint32_t)p;
+    } else {
+        words[w * a.stride + i] = (uint32_t)p;
+    }
+    payload[i] = (uint32_t)i;
+}
+
+// per-word AND / OR over all rows -> res[2*w] (and), res[2*w+1] (or)
+__global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words, uint64_t n,
+                                              uint64_t stride, uint32_t *__restrict__ res) {
+    const uint32_t w = blockIdx.y;
+    uint32_t va = 0xFFFFFFFFu, vo = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
+        uint32_t v = words[w * stride + i];
+        va &= v;
+        vo |= v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        va &= __shfl_xor(va, o);
+        vo |= __shfl_xor(vo, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAnd(&res[2 * w], va);
+        atomicOr(&res[2 * w + 1], vo);
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_init_andor(uint32_t *res, uint32_t nw) {
+    uint32_t t = threadIdx.x;
+    if (t < nw) {
+        res[2 * t] = 0xFFFFFFFFu;
+        res[2 * t + 1] = 0;
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ dw, uint32_t shift,
+                                                   uint64_t n, uint32_t nblocks,
+                                                   uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+#pragma unroll 4
+    for (int j = 0; j < IPT; ++j) {
+        uint64_t i = base + (uint64_t)j * TB + threadIdx.x;
+        if (i < n) atomicAdd(&h[(dw[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan in place over m u32 values, one block of 1024 threads
+__global__ __launch_bounds__(1024) void k_scan_inplace(uint32_t *__restrict__ v, uint64_t m) {
+    __shared__ uint32_t part[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t b = threadIdx.x * per, e = min(m, b + per);
+    uint32_t s = 0;
+    for (uint64_t i = b; i < e; ++i) s += v[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        uint32_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (uint64_t i = b; i < e; ++i) {
+        uint32_t c = v[i];
+        v[i] = run;
+        run += c;
+    }
+}
+
+struct ScatterArgs {
+    const uint32_t *in[MAXW];
+    uint32_t *out[MAXW];
+    uint32_t nlive;
+    uint32_t dword;      // index into in[] of the digit word
+    uint32_t shift;
+    uint32_t nblocks;
+    uint64_t n;
+    const uint32_t *pin;
+    uint32_t *pout;
+    const uint32_t *off;  // scanned hist [256][nblocks]
+};
+
+__global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
+    __shared__ uint32_t base[256], running[256];
+    __shared__ uint32_t wcnt[TB / 64][256], wpre[TB / 64][256];
+    const uint32_t t = threadIdx.x, wave = t >> 6;
+    base[t] = a.off[(uint64_t)t * a.nblocks + blockIdx.x];
+    running[t] = 0;
+    for (int w = 0; w < TB / 64; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+    const uint32_t *dw = a.in[a.dword];
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t i = tbase + (uint64_t)j * TB + t;
+        const bool valid = i < a.n;
+        const uint32_t d = valid ? (dw[i] >> a.shift) & 255u : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t rank = __popcll(peers & lanemask_lt());
+        if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
+        __syncthreads();
+        {
+            uint32_t r = running[t];
+#pragma unroll
+            for (int w = 0; w < TB / 64; ++w) {
+                wpre[w][t] = r;
+                r += wcnt[w][t];
+                wcnt[w][t] = 0;
+            }
+            running[t] = r;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint64_t pos = (uint64_t)base[d] + wpre[wave][d] + rank;
+            for (uint32_t w = 0; w < a.nlive; ++w) a.out[w][pos] = a.in[w][i];
+            a.pout[pos] = a.pin[i];
+        }
+    }
+}
+
+}  // namespace
+
+int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
+                     const uint64_t *pos, bool pos_not, const uint8_t *valid,
+                     uint32_t *out_perm, uint32_t limit) {
+    if (nrows == 0) return IGX_OK;
+    if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
+    if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than 8 keys");
+    ComposeArgs ca{};
+    uint32_t KW = valid ? 1 : 0;
+    for (uint32_t k = 0; k < nkeys; ++k) {
+        ca.ptr[k] = keys[k].ptr;
+        ca.width[k] = keys[k].width;
+        ca.kind[k] = keys[k].kind;
+        ca.desc[k] = keys[k].desc_eff;
+        ca.words[k] = keys[k].words;
+        KW += keys[k].words;
+    }
+    const uint32_t pos_words = (pos == nullptr) ? 1 : 2;
+    KW += pos_words;
+    if (KW > MAXW) return igx_fail(ctx, IGX_ENOTSUP, "sort: composed key too wide");
+    ca.nkeys = nkeys;
+    ca.has_nil = valid ? 1 : 0;
+    ca.pos_words = pos_words;
+    ca.pos_not = pos_not ? 1 : 0;
+    ca.pos = pos;
+    ca.valid = valid;
+    ca.n = nrows;
+    const uint64_t stride = igx_align(nrows, 64);
+    ca.stride = stride;
+
+    const uint32_t nblocks = (uint32_t)((nrows + TILE - 1) / TILE);
+    const size_t words_b = igx_align((size_t)KW * stride * 4, 256);
+    const size_t pay_b = igx_align(stride * 4, 256);
+    const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256);
+    const size_t res_b = igx_align((size_t)KW * 8, 256);
+    void *s;
+    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b, &s);
+    if (rc) return rc;
+    char *c = reinterpret_cast<char *>(s);
+    uint32_t *W[2] = {reinterpret_cast<uint32_t *>(c), reinterpret_cast<uint32_t *>(c + words_b)};
+    uint32_t *P[2] = {reinterpret_cast<uint32_t *>(c + 2 * words_b),
+                      reinterpret_cast<uint32_t *>(c + 2 * words_b + pay_b)};
+    uint32_t *hist = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b);
+    uint32_t *res = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b);
+
+    const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
+    hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
+    hipLaunchKernelGGL(k_init_andor, dim3(1), dim3(TB), 0, ctx->stream, res, KW);
+    const uint32_t ablocks = (uint32_t)std::min<uint64_t>(64, (nrows + TB - 1) / TB);
+    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, res);
+    uint32_t *hres;
+    rc = igx_pinned(ctx, KW * 8, reinterpret_cast<void **>(&hres));
+    if (rc) return rc;
+    IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+
+    // digit plan: word w (0 = most significant), byte b (0 = least significant in word)
+    std::vector<int> live_word(KW, 0);
+    for (uint32_t w = 0; w < KW; ++w) live_word[w] = (hres[2 * w] ^ hres[2 * w + 1]) != 0;
+    int cur = 0;
+    for (int w = (int)KW - 1; w >= 0; --w) {
+        uint32_t diff = hres[2 * w] ^ hres[2 * w + 1];
+        if (!diff) continue;
+        // live words for passes on word w: all w' <= w with any variation
+        ScatterArgs sa{};
+        uint32_t nl = 0;
+        uint32_t dslot = 0;
+        for (int v = 0; v <= w; ++v) {
+            if (!live_word[v]) continue;
+            if (v == w) dslot = nl;
+            sa.in[nl] = W[cur] + (uint64_t)v * stride;
+            sa.out[nl] = W[cur ^ 1] + (uint64_t)v * stride;
+            ++nl;
+        }
+        sa.nlive = nl;
+        sa.dword = dslot;
+        sa.nblocks = nblocks;
+        sa.n = nrows;
+        sa.off = hist;
+        for (int b = 0; b < 4; ++b) {
+            if (((diff >> (8 * b)) & 255u) == 0) continue;
+            sa.shift = 8 * b;
+            sa.pin = P[cur];
+            sa.pout = P[cur ^ 1];
+            hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(TB), 0, ctx->stream,
+                               sa.in[dslot], sa.shift, nrows, nblocks, hist);
+            hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, ctx->stream, hist,
+                               (uint64_t)256 * nblocks);
+            hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+            // swap buffers: the next pass reads what this one wrote
+            cur ^= 1;
+            for (uint32_t l = 0; l < nl; ++l) {
+                const uint32_t *tmp = sa.in[l];
+                sa.in[l] = sa.out[l];
+                sa.out[l] = const_cast<uint32_t *>(tmp);
+            }
+        }
+        live_word[w] = 0;   // never read again below this point
+    }
+    const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+    IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[cur], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}

@@ -1,0 +1,224 @@
+"""Thin tensor-level wrappers over the igx C ABI (device tensors in, device tensors out).
+
+The reference-shaped API (columns / filter / sort / group / top / gadgets) is built on
+these.  Everything here enqueues libigx.so kernels on torch's current stream.
+"""
+import ctypes as C
+import math
+
+from . import _abi
+from ._abi import Agg, Col, Pred, SortKey, TableView, IgxError
+from .runtime import context, ptr, col_of, dtype_kind, torch_mod
+
+# ------------------------------------------------------------------------------------
+# synthetic streams; bit-identical with the CPU oracle
+# ------------------------------------------------------------------------------------
+TCP_FIELDS = (("saddr", "u8x16"), ("daddr", "u8x16"), ("mntns", "u64"), ("pid", "u32"),
+              ("comm", "u8x16"), ("lport", "u16"), ("dport", "u16"), ("family", "u16"),
+              ("size", "u32"), ("dir", "u8"))
+OPEN_FIELDS = (("pid", "u32"), ("uid", "u32"), ("mntns", "u64"), ("comm", "u8x16"),
+               ("ret", "i64"), ("fd", "i64"), ("err", "i64"), ("path", "u32"))
+BIO_FIELDS = (("dev", "u32"), ("cont", "u32"), ("delta", "i64"))
+NP_FIELDS = (("src", "u32"), ("peer", "u32"), ("port", "u16"), ("pkt", "u8"), ("type", "u8"),
+             ("proto", "u8"), ("hostip", "u32"), ("raddr", "u32"))
+FILE_FIELDS = (("inode", "u64"), ("dev", "u32"), ("pid", "u32"), ("tid", "u32"), ("op", "u8"),
+               ("count", "u32"))
+
+
+def _alloc(fields, n, device):
+    torch = torch_mod()
+    dt = {"u8": torch.uint8, "u16": torch.uint16, "u32": torch.uint32, "u64": torch.uint64,
+          "i64": torch.int64}
+    out = {}
+    for name, f in fields:
+        if f == "u8x16":
+            out[name] = torch.empty((n, 16), dtype=torch.uint8, device=device)
+        else:
+            out[name] = torch.empty(n, dtype=dt[f], device=device)
+    return out
+
+
+def perm_params(G):
+    A = 999983
+    while math.gcd(A, G) != 1:
+        A += 2
+    return (A % G, 12345 % G) if G > 1 else (1, 0)
+
+
+def gen_tcp(seed, rank, G, cdf, base, n, out=None):
+    ctx = context()
+    ev = out or _alloc(TCP_FIELDS, n, cdf.device)
+    A, B = perm_params(G)
+    ctx.check(ctx.L.igx_gen_tcp(ctx.h, seed, rank, G, A, B, ptr(cdf), base, n,
+                                *[ptr(ev[k]) for k, _ in TCP_FIELDS]))
+    return ev
+
+
+def gen_open(seed, comm_cdf, base, n):
+    ctx = context()
+    ev = _alloc(OPEN_FIELDS, n, comm_cdf.device)
+    ctx.check(ctx.L.igx_gen_open(ctx.h, seed, ptr(comm_cdf), base, n,
+                                 *[ptr(ev[k]) for k, _ in OPEN_FIELDS]))
+    return ev
+
+
+def gen_bio(seed, q, base, n):
+    ctx = context()
+    ev = _alloc(BIO_FIELDS, n, q.device)
+    ctx.check(ctx.L.igx_gen_bio(ctx.h, seed, ptr(q), q.numel() - 1, base, n,
+                                *[ptr(ev[k]) for k, _ in BIO_FIELDS]))
+    return ev
+
+
+def gen_np(seed, nsrc, npeer, base, n, device="cuda"):
+    ctx = context()
+    ev = _alloc(NP_FIELDS, n, device)
+    ctx.check(ctx.L.igx_gen_np(ctx.h, seed, nsrc, npeer, base, n,
+                               *[ptr(ev[k]) for k, _ in NP_FIELDS]))
+    return ev
+
+
+def gen_file(seed, rank, G, cdf, base, n):
+    ctx = context()
+    ev = _alloc(FILE_FIELDS, n, cdf.device)
+    A, B = perm_params(G)
+    ctx.check(ctx.L.igx_gen_file(ctx.h, seed, rank, G, A, B, ptr(cdf), base, n,
+                                 *[ptr(ev[k]) for k, _ in FILE_FIELDS]))
+    return ev
+
+
+# ------------------------------------------------------------------------------------
+# filter
+# ------------------------------------------------------------------------------------
+def filter_rows(cols, preds, n, valid=None):
+    """cols: list of device tensors (indexed by Pred.col); preds: list of Pred.
+    Returns (idx u32 tensor of length n_selected)."""
+    torch = torch_mod()
+    ctx = context()
+    dev = cols[0].device if cols else "cuda"
+    ccols = (Col * max(1, len(cols)))(*[col_of(t, dtype_kind(t)) for t in cols])
+    cpreds = (Pred * max(1, len(preds)))(*preds)
+    out = torch.empty(max(1, n), dtype=torch.uint32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.uint64, device=dev)
+    ctx.check(ctx.L.igx_filter(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n,
+                               ptr(out), ptr(cnt)))
+    k = int(cnt.item())
+    return out[:k]
+
+
+# ------------------------------------------------------------------------------------
+# sort
+# ------------------------------------------------------------------------------------
+def sort_perm(keys, n, pos=None, valid=None, k=None):
+    """keys: list of (tensor, desc) in sortBy order.  Returns u32 permutation (first k)."""
+    torch = torch_mod()
+    ctx = context()
+    dev = keys[0][0].device if keys else (pos.device if pos is not None else "cuda")
+    sk = []
+    for key in keys:
+        t, desc = key[0], key[1]
+        kind = key[2] if len(key) > 2 else dtype_kind(t)
+        width = t.shape[1] if t.dim() == 2 else t.element_size()
+        sk.append(SortKey(C.c_void_p(t.data_ptr()), width, kind, 1 if desc else 0, 0))
+    arr = (SortKey * max(1, len(sk)))(*sk)
+    m = n if k is None else min(k, n)
+    out = torch.empty(max(1, m), dtype=torch.uint32, device=dev)
+    if n == 0:
+        return out[:0]
+    if k is None:
+        ctx.check(ctx.L.igx_sort_perm(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(out)))
+    else:
+        if valid is not None:
+            raise ValueError("topk does not take a nil mask")
+        ctx.check(ctx.L.igx_topk(ctx.h, arr, len(sk), n, ptr(pos), m, ptr(out)))
+    return out[:m]
+
+
+sort_perm_kinds = sort_perm
+
+
+# ------------------------------------------------------------------------------------
+# group-by table
+# ------------------------------------------------------------------------------------
+class Table:
+    """igx_table: keyed aggregation with first-occurrence tracking."""
+
+    def __init__(self, key_widths, aggs, capacity):
+        self.ctx = context()
+        kw = (C.c_uint32 * len(key_widths))(*key_widths)
+        ca = (Agg * max(1, len(aggs)))(*aggs)
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.L.igx_groupby_create(self.ctx.h, kw, len(key_widths), ca,
+                                                     len(aggs), capacity, C.byref(h)))
+        self.h = h
+        self.key_widths = list(key_widths)
+        self.naggs = len(aggs)
+        self.capacity = capacity
+
+    def update(self, cols, key_cols, n, base_idx=0, preds=()):
+        ctx = self.ctx
+        ctx.bind_stream()
+        ccols = (Col * len(cols))(*[col_of(t, dtype_kind(t)) for t in cols])
+        kc = (C.c_uint32 * len(key_cols))(*key_cols)
+        cp = (Pred * max(1, len(preds)))(*preds)
+        ctx.check(ctx.L.igx_groupby_update(self.h, ccols, len(cols), kc, cp, len(preds), n,
+                                           base_idx))
+
+    def reset(self):
+        self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
+
+    def finalize(self):
+        """Synchronises.  Returns dict of device tensors (views into the table):
+        keys (G, key_stride) u8, aggs list of (G,) u64, first (G,) u64, n_groups."""
+        torch = torch_mod()
+        v = TableView()
+        self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
+        G = v.n_groups
+        return {"n_groups": G, "key_bytes": v.key_bytes, "key_stride": v.key_stride,
+                "keys_ptr": v.keys, "aggs_ptr": [v.aggs[i] for i in range(v.naggs)],
+                "first_ptr": v.first_idx, "d_n_groups": v.d_n_groups}
+
+    def destroy(self):
+        if self.h:
+            self.ctx.L.igx_groupby_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def table_tensors(tab, fin):
+    """Copy the finalized table (device -> device) into torch tensors:
+    keys (G, key_stride) u8, aggs [ (G,) u64 ], first (G,) u64."""
+    torch = torch_mod()
+    ctx = tab.ctx
+    dev = torch.device("cuda", torch.cuda.current_device())
+    G = fin["n_groups"]
+    keys = torch.empty((G, fin["key_stride"]), dtype=torch.uint8, device=dev)
+    aggs = [torch.empty(G, dtype=torch.uint64, device=dev) for _ in fin["aggs_ptr"]]
+    first = torch.empty(G, dtype=torch.uint64, device=dev)
+    if G:
+        ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(keys), C.c_void_p(fin["keys_ptr"]),
+                                       G * fin["key_stride"]))
+        for t, p in zip(aggs, fin["aggs_ptr"]):
+            ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(t), C.c_void_p(p), G * 8))
+        ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(first), C.c_void_p(fin["first_ptr"]), G * 8))
+    return keys, aggs, first
+
+
+# ------------------------------------------------------------------------------------
+# log2 histograms
+# ------------------------------------------------------------------------------------
+def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, hist=None):
+    torch = torch_mod()
+    ctx = context()
+    n = dev.numel()
+    if hist is None:
+        hist = torch.zeros((len(devs) * ncont, nslots), dtype=torch.uint32, device=dev.device)
+    hd = (C.c_uint32 * len(devs))(*devs)
+    ctx.check(ctx.L.igx_hist_log2(ctx.h, ptr(dev), ptr(cont), ptr(delta), n, hd, len(devs),
+                                  ncont, divisor, nslots, ptr(hist)))
+    return hist

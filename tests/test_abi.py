@@ -1,0 +1,126 @@
+"""CPU checks of the C ABI: libigx.so loads, exports every symbol include/igx.h declares,
+and the host-only entry points (filter parser, sort planner) match the reference's rules.
+No compute call is made here (no GPU in the build container)."""
+import ctypes as C
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "igx.h")).read()
+    return sorted(set(re.findall(r"\b(igx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(igx):
+    so = igx._abi.LIB_PATH
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so]).decode()
+    exported = set(re.findall(r" T (igx_[a-z0-9_]+)", out))
+    declared = _declared()
+    assert declared and set(declared) <= exported, set(declared) - exported
+    # and the ctypes mirror covers them all
+    assert set(declared) == {s[0] for s in igx._abi.SIGNATURES}
+
+
+def test_version(igx):
+    assert igx.lib().igx_version() == 1
+
+
+def test_open_without_gpu_fails_cleanly(igx):
+    h = C.c_void_p()
+    rc = igx.lib().igx_open(0, 0, C.byref(h))
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if not has_gpu:
+        assert rc == igx._abi.IGX_ENOENT and not h.value
+
+
+def _filter_cols(igx):
+    d = json.load(open(os.path.join(GOLDEN, "filter_table.json")))
+    fields = []
+    for name, kind in d["columns"]:
+        fields.append((name, kind, 16) if kind == "string" else (name, kind))
+    return d, igx.columns.Columns(fields)
+
+
+def test_parser_golden_errors(igx, oracle):
+    """filter_test.go:129-248: every row's expectError from the C++ parser; the compiled
+    reference value equals the oracle restatement's."""
+    d, cols = _filter_cols(igx)
+    ocols = {}
+    for name, kind in d["columns"]:
+        cls, w = oracle.KIND_CLASS[kind]
+        ocols[name] = oracle.OCol(name, kind, 16 if cls == "string" else w)
+    for row in d["rows"]:
+        try:
+            spec = igx.filter.GetFilterFromString(cols, row["filter"])
+            err = False
+        except igx.filter.FilterError:
+            err = True
+        assert err == row["error"], row
+        if err:
+            continue
+        o = oracle.parse_filter(ocols, row["filter"])
+        assert bool(spec.pred.negate) == o.negate
+        if o.op == "regex":
+            assert spec.pred.cmp == igx._abi.CMP_REGEX
+            continue
+        assert spec.pred.cmp == {"eq": 0, "lt": 2, "le": 3, "gt": 4, "ge": 5}[o.op]
+        ref = bytes(spec.pred.ref[: spec.pred.ref_len])
+        if o.col.kind == "string":
+            assert ref == o.ref.rstrip(b"\0") or ref == o.ref
+        else:
+            assert ref == o.ref, row
+
+
+def test_parser_messages(igx):
+    d, cols = _filter_cols(igx)
+    with pytest.raises(igx.filter.FilterError, match='column "nope" not found'):
+        igx.filter.GetFilterFromString(cols, "nope:1")
+    with pytest.raises(igx.filter.FilterError, match='tried to compare "x" to int column "int"'):
+        igx.filter.GetFilterFromString(cols, "int:x")
+    with pytest.raises(igx.filter.FilterError, match='invalid filter "int:x"'):
+        igx.filter.GetFiltersFromStrings(cols, ["int:1", "int:x"])
+    with pytest.raises(igx.filter.FilterError, match="non-string column"):
+        igx.filter.GetFilterFromString(cols, "int:~1")
+    # Convert() truncation: int8:300 -> 44
+    s = igx.filter.GetFilterFromString(cols, "int8:300")
+    assert s.pred.ref[0] == 44
+    s = igx.filter.GetFilterFromString(cols, "INT8:!-1")      # column names are case-insensitive
+    assert s.negate and s.pred.ref[0] == 0xFF
+    s = igx.filter.GetFilterFromString(cols, "string:>=!x")   # '!' after the operator is value
+    assert not s.negate and bytes(s.pred.ref[:2]) == b"!x"
+
+
+def test_sort_prepare_tables(igx):
+    """sort_test.go:176-231: CanSortBy / FilterSortableColumns truth tables."""
+    cols = igx.columns.Columns([("embeddedInt", "int"), ("int", "int"), ("uint", "uint"),
+                                ("string", "string", 16), ("float32", "float32"),
+                                ("float64", "float64"), ("bool", "bool"),
+                                ("group", "string", 16), ("extractor", "int")])
+    cols.SetExtractor("extractor", lambda r: str(r))
+    cols.AddColumn("virtual_column", lambda r: "")
+    S = igx.sort
+    assert S.CanSortBy(cols, ["uint"])
+    assert S.CanSortBy(cols, ["extractor"])
+    assert not S.CanSortBy(cols, ["virtual_column"])
+    assert not S.CanSortBy(cols, ["non_existent_column"])
+    assert S.FilterSortableColumns(cols, ["uint"]) == (["uint"], [])
+    assert S.FilterSortableColumns(cols, ["virtual_column"]) == ([], ["virtual_column"])
+    assert S.FilterSortableColumns(cols, ["uint", "extractor"]) == (["uint", "extractor"], [])
+    assert S.FilterSortableColumns(cols, ["", "-uint", "x"]) == (["-uint"], ["", "x"])
+    keys = S.Prepare(cols, ["-extractor", "bool", "uint"]).keys
+    assert [k.desc for k in keys] == [1, 0, 0]
+    # extractor columns sort by the raw field kind (sort.go:46-48)
+    assert keys[0].kind == igx._abi.KIND_INT
+    assert keys[1].kind == igx._abi.KIND_BOOL

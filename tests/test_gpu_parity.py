@@ -1,0 +1,189 @@
+"""GPU parity: libigx.so (through the C ABI) vs the CPU oracle on identical seeded streams.
+
+Bit-exact for everything (integer counting, keying and ordering).  Sizes are chosen so
+the oracle finishes in seconds; full-size runs are covered by the property tests in
+tests/test_gpu_properties.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+    return T
+
+
+@pytest.fixture(scope="module")
+def E(igx):
+    return igx.engine
+
+
+@pytest.fixture(scope="module")
+def H(igx):
+    return igx.columns
+
+
+def _h(H, d):
+    return {k: H.host(v) for k, v in d.items()}
+
+
+def test_gen_tcp_bit_exact(oracle, E, H, torch):
+    G, n = 5000, 200_000
+    cdf = oracle.zipf_cdf(G, 1.1)
+    for rank, base in [(0, 0), (3, 123_456_789)]:
+        ref = oracle.gen_tcp(0xC2, rank, G, cdf, base, n)
+        got = _h(H, E.gen_tcp(0xC2, rank, G, H.to_device(cdf), base, n))
+        for k in ref:
+            assert np.array_equal(ref[k], got[k]), k
+
+
+def test_gen_others_bit_exact(oracle, E, H, torch):
+    n = 100_000
+    ccdf = oracle.zipf_cdf(64, 1.0)
+    ref = oracle.gen_open(0xC1, ccdf, 7, n)
+    got = _h(H, E.gen_open(0xC1, H.to_device(ccdf), 7, n))
+    for k in ref:
+        assert np.array_equal(ref[k], got[k]), k
+    q = oracle.lognormal_quantiles(np.log(2e5), 1.5)
+    ref = oracle.gen_bio(0xC3, q, 11, n)
+    got = _h(H, E.gen_bio(0xC3, H.to_device(q), 11, n))
+    for k in ref:
+        assert np.array_equal(ref[k].view(np.uint64), got[k].view(np.uint64)), k
+    ref = oracle.gen_np(0xC4, 10_000, 100_000, 5, n)
+    got = _h(H, E.gen_np(0xC4, 10_000, 100_000, 5, n))
+    for k in ref:
+        assert np.array_equal(ref[k], got[k]), k
+    fcdf = oracle.zipf_cdf(20_000, 1.05)
+    ref = oracle.gen_file(0xC5, 2, 20_000, fcdf, 9, n)
+    got = _h(H, E.gen_file(0xC5, 2, 20_000, H.to_device(fcdf), 9, n))
+    for k in ref:
+        assert np.array_equal(ref[k], got[k]), k
+
+
+TCP_KEY = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family")
+
+
+def _tcp_table(E, igx, ev, n, capacity, base=0):
+    A = igx._abi
+    cols = [ev[k] for k in TCP_KEY] + [ev["size"], ev["dir"]]
+    widths = [16, 16, 8, 4, 16, 2, 2, 2]
+    aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
+    tab = E.Table(widths, aggs, capacity)
+    tab.update(cols, list(range(8)), n, base)
+    return tab
+
+
+def _unpad_tcp_keys(keys):
+    # device key layout: every column padded to 4 bytes: 16,16,8,4,16,4,4,4 (72 B)
+    k = keys[:, :72]
+    return np.concatenate([k[:, :60], k[:, 60:62], k[:, 64:66], k[:, 68:70]], axis=1)
+
+
+@pytest.mark.parametrize("G,n", [(1000, 300_000), (200_000, 400_000)])
+def test_groupby_top_tcp(oracle, E, H, igx, torch, G, n):
+    cdf = oracle.zipf_cdf(G, 1.1)
+    ev_h = oracle.gen_tcp(0xC2, 0, G, cdf, 0, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    tab = _tcp_table(E, igx, ev, n, capacity=2 * G, base=1000)
+    fin = tab.finalize()
+    keys, aggs, first = E.table_tensors(tab, fin)
+    gk = _unpad_tcp_keys(H.host(keys))
+    gs, gr, gf = H.host(aggs[0]), H.host(aggs[1]), H.host(first)
+    okeys, oaggs, ofirst = oracle.groupby(
+        oracle.pack_cols(ev_h, TCP_KEY),
+        [{"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 0},
+         {"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 1}],
+        base_idx=1000)
+    assert fin["n_groups"] == len(okeys)
+    ref = {bytes(k): (int(s), int(r), int(f)) for k, s, r, f in zip(okeys, oaggs[0], oaggs[1], ofirst)}
+    got = {bytes(k): (int(s), int(r), int(f)) for k, s, r, f in zip(gk, gs, gr, gf)}
+    assert got == ref
+    tab.destroy()
+
+
+def test_topk_matches_go_sort(oracle, E, H, igx, torch):
+    """top tcp: nextStats -> SortStats(["-sent","-recv"]) -> stats[:20]."""
+    G, n = 20_000, 500_000
+    cdf = oracle.zipf_cdf(G, 1.1)
+    ev_h = oracle.gen_tcp(0xC2, 0, G, cdf, 0, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    tab = _tcp_table(E, igx, ev, n, capacity=2 * G)
+    fin = tab.finalize()
+    keys, aggs, first = E.table_tensors(tab, fin)
+    Gn = fin["n_groups"]
+    top = E.sort_perm([(aggs[0], True), (aggs[1], True)], Gn, pos=first, k=20)
+    got = H.host(first)[H.host(top).astype(np.int64)]
+    Gref, okeys, osent, orecv, ofirst = oracle.top_tcp(ev_h, 20)
+    assert Gn == Gref
+    assert list(got) == list(ofirst)
+    # full sort too, against the Go SliceStable restatement on first-occurrence order
+    full = H.host(E.sort_perm([(aggs[0], True), (aggs[1], True)], Gn, pos=first))
+    fh = H.host(first)
+    order = np.argsort(fh, kind="stable")           # canonical pre-sort order
+    sent, recv = H.host(aggs[0])[order], H.host(aggs[1])[order]
+    perm = oracle.go_sort_entries([(sent, "uint64", True), (recv, "uint64", True)], Gn)
+    assert np.array_equal(fh[full.astype(np.int64)], fh[order][perm.astype(np.int64)])
+
+
+def test_ties_and_parity(oracle, E, H, torch):
+    """Heavy ties, 1-3 keys, mixed directions, signed/unsigned/bytes: exact Go order."""
+    rng = np.random.default_rng(7)
+    for trial in range(12):
+        n = int(rng.integers(1, 5000))
+        nk = int(rng.integers(1, 4))
+        kinds = rng.choice(["int8", "int64", "uint16", "uint64", "string", "int32"], nk)
+        cols_h, keys_d, keys_o = [], [], []
+        for kd in kinds:
+            desc = bool(rng.random() < 0.6)
+            if kd == "string":
+                a = np.zeros((n, 8), np.uint8)
+                a[:, 0] = rng.integers(97, 100, n)
+                a[:, 1] = rng.integers(0, 2, n) * 98
+            else:
+                a = rng.integers(-3 if kd.startswith("int") else 0, 3, n).astype(kd)
+            keys_d.append((H.to_device(a), desc))
+            keys_o.append((a, kd, desc))
+        got = H.host(E.sort_perm(keys_d, n))
+        ref = oracle.go_sort_entries(keys_o, n)
+        assert np.array_equal(got, ref), (trial, kinds)
+
+
+def test_filter_c1(oracle, E, H, igx, torch):
+    """C1: FilterEntries(["err:0", "pid:>=1000"]) then SortEntries(["comm", "-pid"])."""
+    n = 1_000_000
+    ccdf = oracle.zipf_cdf(64, 1.0)
+    ev_h = oracle.gen_open(0xC1, ccdf, 0, n)
+    cols = igx.columns.Columns([("pid", "uint32"), ("uid", "uint32"), ("mntns", "uint64"),
+                                ("comm", "string", 16), ("ret", "int64"), ("fd", "int64"),
+                                ("err", "int64"), ("path", "uint32")])
+    batch = igx.columns.EventBatch(cols, {k: H.to_device(v) for k, v in ev_h.items()})
+    out = igx.filter.FilterEntries(cols, batch, ["err:0", "pid:>=1000"])
+    ocols = {"err": oracle.OCol("err", "int64", 8), "pid": oracle.OCol("pid", "uint32", 4)}
+    sel = oracle.match_rows([oracle.parse_filter(ocols, "err:0"),
+                             oracle.parse_filter(ocols, "pid:>=1000")], ev_h)
+    assert out.n == len(sel)
+    assert np.array_equal(H.host(out["pid"]), ev_h["pid"][sel])
+    srt = igx.sort.SortEntries(cols, out, ["comm", "-pid"])
+    perm = oracle.go_sort_entries([(ev_h["comm"][sel], "string", False),
+                                   (ev_h["pid"][sel], "uint32", True)], len(sel))
+    assert np.array_equal(H.host(srt["pid"]), ev_h["pid"][sel][perm])
+    assert np.array_equal(H.host(srt["comm"]), ev_h["comm"][sel][perm])
+
+
+def test_hist_log2_c3(oracle, E, H, torch):
+    n = 2_000_000
+    q = oracle.lognormal_quantiles(np.log(2e5), 1.5)
+    ev_h = oracle.gen_bio(0xC3, q, 0, n)
+    devs = [(8 << 20) | (16 * k) for k in range(16)]
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    got = H.host(E.hist_log2(ev["dev"], ev["cont"], ev["delta"].view(torch.int64), devs, 256))
+    ref = oracle.hist_log2(ev_h["dev"], ev_h["cont"], ev_h["delta"], devs, 256)
+    assert got.shape == (4096, 27)
+    assert np.array_equal(got, ref)
+    # reference shape: single key (no per-disk / per-container keys), 27 slots
+    got1 = H.host(E.hist_log2(ev["dev"], None, ev["delta"].view(torch.int64), devs[:1], 1))
+    ref1 = oracle.hist_log2(ev_h["dev"], np.zeros(n, np.uint32), ev_h["delta"], devs[:1], 1)
+    assert np.array_equal(got1, ref1)
