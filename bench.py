@@ -91,14 +91,10 @@ def main():
         if record:
             ev1.record()
         fin = tab.finalize()                          # syncs: group count for the top-K
-        keys_p = fin["keys_ptr"]
-        sent = fin["aggs_ptr"][0]
-        recv = fin["aggs_ptr"][1]
-        first = fin["first_ptr"]
         Gn = fin["n_groups"]
-        idx = topk_raw(E, igx, [(sent, 8, A.KIND_UINT, 1), (recv, 8, A.KIND_UINT, 1)], Gn,
-                       first, K, dev)
-        cand = gather_candidates(igx, tab, idx, dev)
+        # SortStats(["-sent","-recv"]) over the table's groups, first K slots
+        slots = tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K)
+        cand = tab.gather(slots)                      # K rows: key 72 | sent | recv | first
         if world > 1:
             out = [torch.empty_like(cand) for _ in range(world)]
             dist.all_gather(out, cand)
@@ -176,35 +172,6 @@ def main():
     tab.destroy()
     if world > 1:
         dist.destroy_process_group()
-
-
-def topk_raw(E, igx, keys, n, pos_ptr, k, dev):
-    """igx_topk over raw table pointers (no copies)."""
-    import ctypes as C
-    import torch
-    A = igx._abi
-    ctx = igx.runtime.context()
-    sk = (A.SortKey * len(keys))(*[A.SortKey(C.c_void_p(p), w, kind, d, 0)
-                                    for p, w, kind, d in keys])
-    m = min(k, n)
-    out = torch.empty(max(1, m), dtype=torch.int32, device=dev)
-    if m:
-        ctx.check(ctx.L.igx_topk(ctx.h, sk, len(keys), n, C.c_void_p(pos_ptr), m,
-                                 C.c_void_p(out.data_ptr())))
-    return out[:m]
-
-
-def gather_candidates(igx, tab, idx, dev):
-    """Candidate rows (K x 96 B): key 72 | sent 8 | recv 8 | first 8 (igx_groupby_gather)."""
-    import ctypes as C
-    import torch
-    ctx = igx.runtime.context()
-    k = idx.numel()
-    cand = torch.zeros((max(1, k), 96), dtype=torch.uint8, device=dev)
-    if k:
-        ctx.check(ctx.L.igx_groupby_gather(tab.h, C.c_void_p(idx.data_ptr()), k,
-                                           C.c_void_p(cand.data_ptr())))
-    return cand[:k]
 
 
 def merge_candidates(E, H, allc, K):

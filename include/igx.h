@@ -177,16 +177,34 @@ typedef struct {
     uint64_t cond_val;
 } igx_agg;
 
+/* The table is an open-addressing array of n_slots records of key_stride bytes; a group's
+ * id is its slot.  Record of slot s (at keys + s*key_stride): the packed key, then the
+ * slot's first_idx and aggregates at the pointers below + s*key_stride.  groups[0..n_groups)
+ * lists the occupied slots in ascending slot order (the canonical pre-sort order is
+ * first_idx, not this). */
 typedef struct {
     uint64_t n_groups;        /* host copy, valid after igx_groupby_finalize */
+    uint64_t n_slots;
     uint32_t key_bytes;       /* packed key bytes per group (each key column padded to 4) */
-    uint32_t key_stride;      /* bytes between consecutive keys in `keys` */
+    uint32_t key_stride;      /* record size: bytes between consecutive slots */
     uint32_t naggs;
-    const uint8_t *keys;      /* device: n_groups x key_stride */
-    const uint64_t *aggs[16]; /* device: one u64 array per aggregate, indexed by group */
-    const uint64_t *first_idx;/* device: first-occurrence event index per group */
+    const uint8_t *keys;      /* device: slot 0's packed key; n_slots x key_stride */
+    const uint64_t *aggs[16]; /* device: slot 0's aggregate a; stride key_stride */
+    const uint64_t *first_idx;/* device: slot 0's first-occurrence index; stride key_stride */
+    const uint32_t *groups;   /* device: occupied slots, n_groups entries */
     const uint64_t *d_n_groups;/* device: group count */
 } igx_table_view;
+
+/* Sort key over a table's columns (igx_groupby_sort). */
+enum igx_tsrc { IGX_TSRC_AGG = 0, IGX_TSRC_FIRST = 1, IGX_TSRC_KEY = 2 };
+typedef struct {
+    uint32_t src;    /* enum igx_tsrc */
+    uint32_t index;  /* aggregate index (IGX_TSRC_AGG) */
+    uint32_t offset; /* byte offset in the packed key (IGX_TSRC_KEY) */
+    uint32_t width;  /* bytes (IGX_TSRC_KEY) */
+    uint32_t kind;   /* enum igx_kind (IGX_TSRC_KEY) */
+    uint32_t desc;   /* '-' prefix */
+} igx_tsortkey;
 
 /* capacity = maximum number of distinct groups.  key_widths: byte width of each key
  * column (packed, each padded to a multiple of 4). */
@@ -207,7 +225,14 @@ int igx_groupby_finalize(igx_table *t, igx_table_view *view);
  * igx_groupby_finalize.  Asynchronous. */
 int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows);
 int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete loop) */
+/* SortStats over the table's groups (same order as igx_sort_perm with pos = first_idx);
+ * writes the first k (0 = all) group slots to out_slots (device u32).  Call after
+ * igx_groupby_finalize.  Asynchronous. */
+int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uint32_t k,
+                     uint32_t *out_slots);
 int igx_groupby_destroy(igx_table *t);
+/* Diagnostics only (IGX_GB_DEBUG env bit 3): LDS-cache hits / misses since the last call. */
+int igx_groupby_debug_counts(igx_table *t, uint64_t *out4);
 
 /* ---- log2 latency histograms ---------------------------------------------------------- */
 /* hist[(dev_index(dev)*ncont + cont) * nslots + slot] += 1 for every row with delta >= 0

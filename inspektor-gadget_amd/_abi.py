@@ -50,9 +50,18 @@ class Agg(C.Structure):
 
 
 class TableView(C.Structure):
-    _fields_ = [("n_groups", C.c_uint64), ("key_bytes", C.c_uint32), ("key_stride", C.c_uint32),
-                ("naggs", C.c_uint32), ("keys", C.c_void_p), ("aggs", C.c_void_p * 16),
-                ("first_idx", C.c_void_p), ("d_n_groups", C.c_void_p)]
+    _fields_ = [("n_groups", C.c_uint64), ("n_slots", C.c_uint64), ("key_bytes", C.c_uint32),
+                ("key_stride", C.c_uint32), ("naggs", C.c_uint32), ("keys", C.c_void_p),
+                ("aggs", C.c_void_p * 16), ("first_idx", C.c_void_p), ("groups", C.c_void_p),
+                ("d_n_groups", C.c_void_p)]
+
+
+TSRC_AGG, TSRC_FIRST, TSRC_KEY = 0, 1, 2
+
+
+class TSortKey(C.Structure):
+    _fields_ = [("src", C.c_uint32), ("index", C.c_uint32), ("offset", C.c_uint32),
+                ("width", C.c_uint32), ("kind", C.c_uint32), ("desc", C.c_uint32)]
 
 
 class IgxError(RuntimeError):
@@ -89,8 +98,10 @@ SIGNATURES = [
                                 _U32, _U64, _U64]),
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
+    ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
     ("igx_groupby_reset", _I, [_VP]),
     ("igx_groupby_destroy", _I, [_VP]),
+    ("igx_groupby_debug_counts", _I, [_VP, _VP]),
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
     ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),

@@ -474,8 +474,9 @@ extern "C" int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, cons
     return IGX_OK;
 }
 
-static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
-                       const uint64_t *pos, const uint8_t *valid, uint32_t *out, uint32_t limit) {
+static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
+                       uint64_t nrows, const uint64_t *pos, const uint8_t *valid, uint32_t *out, uint32_t limit,
+                       const uint32_t *rowmap, uint32_t pos_stride = 8) {
     if (!ctx) return IGX_EINVAL;
     if (nrows == 0) return IGX_OK;                          // sort.go:36-38
     if (!out) return igx_fail(ctx, IGX_EINVAL, "sort: null output");
@@ -488,6 +489,7 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, ui
         p.ptr = static_cast<const uint8_t *>(k.ptr);
         p.width = k.width;
         p.kind = k.kind;
+        p.stride = strides ? strides[i] : k.width;
         if (!p.ptr) return igx_fail(ctx, IGX_EINVAL, "sort: key %u has no column", i);
         if (k.kind == IGX_KIND_BYTES) {
             p.words = (k.width + 3) / 4;
@@ -505,20 +507,27 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, ui
     if (plan.empty()) {
         // nothing sortable: the slice is left as is (SortEntries with only invalid keys is a no-op)
         // (no pass runs, so nil entries stay where they are too): identity permutation
-        return launch_sort_perm(ctx, nullptr, 0, nrows, nullptr, false, nullptr, out, limit);
+        return launch_sort_perm(ctx, nullptr, 0, nrows, nullptr, false, nullptr, out, limit, rowmap);
     }
-    return launch_sort_perm(ctx, plan.data(), (uint32_t)plan.size(), nrows, pos, parity != 0, valid, out, limit);
+    return launch_sort_perm(ctx, plan.data(), (uint32_t)plan.size(), nrows, pos, parity != 0, valid, out, limit,
+                            rowmap, pos_stride);
+}
+
+int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
+                     uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
+                     uint32_t limit, uint32_t *out) {
+    return sort_common(ctx, keys, strides, nkeys, nrows, pos, nullptr, out, limit, rowmap, pos_stride);
 }
 
 extern "C" int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                              const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm) {
-    return sort_common(ctx, keys, nkeys, nrows, pos, valid, out_perm, 0);
+    return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, valid, out_perm, 0, nullptr);
 }
 
 extern "C" int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                         const uint64_t *pos, uint32_t k, uint32_t *out_idx) {
     if (k == 0) return IGX_OK;
-    return sort_common(ctx, keys, nkeys, nrows, pos, nullptr, out_idx, k);
+    return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, nullptr, out_idx, k, nullptr);
 }
 
 extern "C" int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, const int64_t *delta,

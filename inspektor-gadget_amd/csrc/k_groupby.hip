@@ -7,72 +7,97 @@
 // wrap at their declared width, and each group remembers the global index of its first
 // event -- the canonical pre-sort order that replaces BPF map order.
 //
-// Layout in HBM (one igx_table):
-//   slots[C]   16 B {u64 tag, u32 id, u32 -}  open addressing, linear probing, C = 2^k
-//   keys[G]    key_stride bytes per dense group id (packed key words)
-//   aggs[a][G] u64 per aggregate, first[G] u64, counter u32, err u32
-// A new key claims a slot with a 64-bit CAS on the tag, takes a dense id from a counter,
-// writes its key with write-through (sc1) stores and publishes the id with an sc1 store
-// after `s_waitcnt vmcnt(0)`; readers that hit the same tag poll the id and compare the
-// key with sc1 loads (MI355X_MICROARCH.md §Workgroup dispatch, hand-off table row 1).
+// HBM table: S = 2^k records (S >= 2 x capacity), open addressing with linear probing.
+// One record per slot, laid out so a probe touches ONE cache line (R = 64/128 B):
+//     [0, KOFF)            key words (KW x u32, packed; each key column padded to 4 B)
+//     KOFF                 u64 tag   (hash | 1; 0 = empty)
+//     KOFF + 8             u32 ready (key published)
+//     KOFF + 16            u64 first (first-occurrence event index)
+//     KOFF + 24 + 8a       u64 aggregate a
+// The slot index IS the group id; igx_groupby_finalize lists the occupied slots.
+// A new key claims a record with a 64-bit CAS on the tag, writes its key with write-through
+// (sc1) stores and publishes `ready` with an sc1 store after `s_waitcnt vmcnt(0)`; readers
+// load the record's first KOFF+24 bytes with 16-byte sc1 buffer loads (one round trip)
+// and compare the key in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off
+// table row 1).  No counter is touched per new key.
 //
-// Partial aggregates are staged per workgroup in LDS (direct-mapped on the dense id,
-// first come first served) with LDS u64 atomics; ids that miss go straight to HBM
-// atomics; the LDS cache is committed with HBM atomics when the workgroup finishes.
+// Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 2-way on the key
+// hash, entries hold the full key, its slot and the workgroup's partial aggregates;
+// first come, never evicted, so the Zipf-hot keys settle in LDS and their events cost only
+// their own input bytes plus LDS atomics.  Misses are queued per wave in LDS and resolved
+// 64 at a time against HBM (a wave pays one probe round trip per 64 misses, not one per
+// iteration in which any lane missed).  The cache is committed with HBM atomics at the end.
+#include <cstdlib>
+#include <utility>
+
 #include "k_common.h"
 
 namespace {
 
-constexpr int TB = 256;
-constexpr uint32_t ID_NONE = 0xFFFFFFFFu;
-constexpr uint32_t ID_OVF = 0xFFFFFFFEu;
+constexpr uint32_t SLOT_OVF = 0xFFFFFFFFu;
 constexpr int KWMAX = 32;
-constexpr int AMAX = 8;
+constexpr int AMAX = 4;   // top file needs 4 (reads, rbytes, writes, wbytes)
+constexpr int PMAX = 2;   // more predicates: run igx_filter first
+constexpr int GTB = 1024;
+constexpr uint32_t ST_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t ST_BUSY = 0xFFFFFFFEu;
+constexpr uint32_t QCAP = 128;   // per-wave miss queue (row ids) in LDS
 
-enum KMode : uint32_t { KM_ZERO = 0, KM_U8 = 1, KM_U16 = 2, KM_U32 = 4, KM_X4 = 16, KM_CONT = 17 };
+__host__ __device__ constexpr uint32_t koff_of(int kw) { return (uint32_t)((4 * kw + 7) & ~7); }
+__host__ __device__ constexpr uint32_t rec_bytes(int kw, uint32_t naggs) {
+    const uint32_t b = koff_of(kw) + 24 + 8 * naggs;
+    return b <= 64 ? 64u : ((b + 127) & ~127u);
+}
 
+// Every input byte is fetched with an unconditional load (no load sits behind a runtime
+// branch), so all of a row's loads issue back to back and retire under one wait.
 struct GbArgs {
-    // key words
+    // static layouts: one base pointer per key column
+    const uint8_t *kcol[16];
+    // generic layout: word w = (dword at kptr[w] + row*kwidth[w] + koff[w]) & kmask[w]
     const uint8_t *kptr[KWMAX];
     uint32_t kwidth[KWMAX];
     uint32_t koff[KWMAX];
-    uint32_t kmode[KWMAX];
-    // aggregates
+    uint32_t kmask[KWMAX];
+    // aggregates: value = SUM column (vwidth bytes) or 1 (COUNT), if cond column == cval
     const uint8_t *vptr[AMAX];
     const uint8_t *cptr[AMAX];
     uint64_t cval[AMAX];
-    uint32_t vwidth[AMAX], vsign[AMAX], vcount[AMAX], cwidth[AMAX];
+    uint32_t vwidth[AMAX], vsign[AMAX], vcount[AMAX], cwidth[AMAX], hascond[AMAX];
     uint32_t naggs;
-    uint32_t lds_entries;   // L (power of two)
+    // scalar predicates (FilterSpec on a <= 8-byte column), AND-ed
+    const uint8_t *pptr[PMAX];
+    uint64_t pref[PMAX];
+    uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX];
+    uint32_t npred;
+    uint32_t lds_entries;   // E (power of two)
     // input
     const uint8_t *valid;
     uint64_t n, base_idx;
     // table
-    uint64_t *slots;        // 2 x u64 per slot: [tag][id]
-    uint32_t *keys;
-    uint32_t key_stride_w;
-    uint64_t *aggs[AMAX];
-    uint64_t *first;
-    uint32_t *counter;
+    uint8_t *rec;
+    uint32_t rec_len;       // R
+    uint32_t rec_total;     // S x R (< 2^32)
     uint32_t *err;
     uint64_t mask;
-    uint32_t cap_ids;
     uint32_t max_probe;
+    // diagnostics (IGX_GB_DEBUG, never set in production): bit0 stop after load+hash,
+    // bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count hits/misses
+    uint32_t dbg;
+    unsigned long long *dbg_cnt;
 };
 
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
+// Key hash: one 64-bit multiply per 8 key bytes plus a murmur3 finaliser.  Exactness never
+// depends on it (keys are compared in full); it only spreads slots and LDS sets.
 template <int KW>
 __device__ __forceinline__ uint64_t hash_key(const uint32_t (&k)[KW]) {
     uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)KW;
 #pragma unroll
     for (int w = 0; w < KW; w += 2) {
         uint64_t x = (uint64_t)k[w] | ((w + 1 < KW) ? ((uint64_t)k[w + 1] << 32) : 0ull);
-        x *= 0x87C37B91114253D5ull;
-        x = rotl64(x, 31);
-        x *= 0x4CF5AD432745937Full;
-        h ^= x;
-        h = rotl64(h, 27) * 5 + 0x52DCE729ull;
+        h = rotl64(h ^ (x * 0x9E3779B97F4A7C15ull), 29) + (h << 3);
     }
     h ^= h >> 33;
     h *= 0xFF51AFD7ED558CCDull;
@@ -82,190 +107,529 @@ __device__ __forceinline__ uint64_t hash_key(const uint32_t (&k)[KW]) {
     return h;
 }
 
-template <int KW>
-__device__ __forceinline__ void load_key(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
-#pragma unroll
-    for (int w = 0; w < KW; ++w) {
-        const uint32_t m = a.kmode[w];
-        const uint8_t *p = a.kptr[w];
-        if (m == KM_X4) {
-            if constexpr (true) {
-                if (w + 3 < KW) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(p + row * a.kwidth[w] + a.koff[w]);
-                    k[w] = v.x;
-                    if (w + 1 < KW) k[w + 1] = v.y;
-                    if (w + 2 < KW) k[w + 2] = v.z;
-                    if (w + 3 < KW) k[w + 3] = v.w;
-                }
-            }
-        } else if (m == KM_U32) {
-            k[w] = *reinterpret_cast<const uint32_t *>(p + row * a.kwidth[w] + a.koff[w]);
-        } else if (m == KM_U16) {
-            k[w] = reinterpret_cast<const uint16_t *>(p)[row];
-        } else if (m == KM_U8) {
-            k[w] = p[row];
-        } else if (m == KM_ZERO) {
-            k[w] = 0;
-        }
-    }
+// aligned dword containing byte `off`, shifted so that byte lands in bits 0..7; the
+// dword containing a column's last byte never crosses its last 4-byte block (no overrun)
+__device__ __forceinline__ uint32_t ldw(const uint8_t *base, uint64_t off) {
+    const uint32_t d = *reinterpret_cast<const uint32_t *>(base + (off & ~3ull));
+    return d >> ((uint32_t)(off & 3u) * 8u);
 }
 
-// lookup-or-insert; returns dense id, ID_OVF on overflow
+// zero-extended little-endian value of `width` (1, 2, 4 or 8) bytes at row; branch-free
+__device__ __forceinline__ uint64_t ld_val(const uint8_t *base, uint64_t row, uint32_t width) {
+    const uint64_t b = row * width;
+    const uint32_t lomask = width >= 4 ? 0xFFFFFFFFu : ((1u << (8 * width)) - 1u);
+    const uint32_t lo = ldw(base, b) & lomask;
+    const uint32_t hi = ldw(base, b + (width == 8 ? 4u : 0u));
+    return (uint64_t)lo | ((uint64_t)(width == 8 ? hi : 0u) << 32);
+}
+
+__device__ __forceinline__ uint64_t sext(uint64_t v, uint32_t width) {
+    const uint32_t sh = 64u - 8u * width;
+    return sh ? (uint64_t)(((int64_t)(v << sh)) >> sh) : v;
+}
+
+// Key layouts.  StaticLayout<W...> fixes the key column widths at compile time (the
+// reference's BPF key structs: ip_key_t, file_id, the advisor tuple, single columns), so
+// every key load is one typed load (dwordx4 for a 16-byte column) with no descriptors in
+// registers.  GenericLayout<KW> handles any other layout from per-word descriptors.
+template <int... W>
+struct StaticLayout {
+    static constexpr int NC = sizeof...(W);
+    static constexpr int Ws[NC] = {W...};
+    static constexpr int words(int c) { return (Ws[c] + 3) / 4; }
+    static constexpr int off(int c) {
+        int o = 0;
+        for (int i = 0; i < c; ++i) o += words(i);
+        return o;
+    }
+    static constexpr int KW = off(NC);
+    static constexpr bool is_static = true;
+
+    template <int c>
+    __device__ __forceinline__ static void load_col(const GbArgs &a, uint64_t row, uint32_t *k) {
+        constexpr int w = Ws[c];
+        constexpr int o = off(c);
+        const uint8_t *p = a.kcol[c];
+        if constexpr (w == 16) {
+            const uint4 q = reinterpret_cast<const uint4 *>(p)[row];
+            k[o] = q.x; k[o + 1] = q.y; k[o + 2] = q.z; k[o + 3] = q.w;
+        } else if constexpr (w == 8) {
+            const uint2 q = reinterpret_cast<const uint2 *>(p)[row];
+            k[o] = q.x; k[o + 1] = q.y;
+        } else if constexpr (w == 4) {
+            k[o] = reinterpret_cast<const uint32_t *>(p)[row];
+        } else if constexpr (w == 2) {
+            k[o] = reinterpret_cast<const uint16_t *>(p)[row];
+        } else if constexpr (w == 1) {
+            k[o] = p[row];
+        } else {
+            static_assert(w % 4 == 0, "key widths other than 1/2 must be multiples of 4");
+#pragma unroll
+            for (int j = 0; j < w / 4; ++j) k[o + j] = reinterpret_cast<const uint32_t *>(p + row * w)[j];
+        }
+    }
+    template <size_t... I>
+    __device__ __forceinline__ static void load_all(const GbArgs &a, uint64_t row, uint32_t *k,
+                                                    std::index_sequence<I...>) {
+        (load_col<(int)I>(a, row, k), ...);
+    }
+    __device__ __forceinline__ static void load(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
+        load_all(a, row, k, std::make_index_sequence<NC>{});
+    }
+};
+
+template <int KWG>
+struct GenericLayout {
+    static constexpr int KW = KWG;
+    static constexpr bool is_static = false;
+    __device__ __forceinline__ static void load(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
+#pragma unroll
+        for (int w = 0; w < KW; ++w) k[w] = ldw(a.kptr[w], row * a.kwidth[w] + a.koff[w]) & a.kmask[w];
+    }
+};
+
+// FilterSpec on a scalar column, evaluated on an already loaded value
+// (getComparisonFuncForComparisonType, filter.go:236-263: (field OP ref) != negate).
+__device__ __forceinline__ bool pred_scalar(uint64_t v, uint64_t ref, uint32_t width, uint32_t kind,
+                                            uint32_t cmp, uint32_t neg) {
+    int c;
+    if (kind == IGX_KIND_FLOAT) {
+        double x, y;
+        if (width == 4) {
+            x = __uint_as_float((uint32_t)v);
+            y = __uint_as_float((uint32_t)ref);
+        } else {
+            x = __longlong_as_double((long long)v);
+            y = __longlong_as_double((long long)ref);
+        }
+        c = (x != x || y != y) ? 2 : (x < y ? -1 : (x > y ? 1 : 0));
+    } else if (kind == IGX_KIND_INT) {
+        const int64_t x = (int64_t)sext(v, width), y = (int64_t)sext(ref, width);
+        c = x < y ? -1 : (x > y ? 1 : 0);
+    } else {
+        c = v < ref ? -1 : (v > ref ? 1 : 0);
+    }
+    bool r = c != 2 && ((cmp == IGX_CMP_EQ && c == 0) || (cmp == IGX_CMP_LT && c < 0) ||
+                        (cmp == IGX_CMP_LE && c <= 0) || (cmp == IGX_CMP_GT && c > 0) ||
+                        (cmp == IGX_CMP_GE && c >= 0));
+    return r != (neg != 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const GbArgs &a) {
+    return __builtin_amdgcn_make_buffer_rsrc(a.rec, (short)0, (int)a.rec_total, 0x00020000);
+}
+
+// lookup-or-insert in the HBM table; returns the slot (SLOT_OVF: table full).  *first_seen
+// receives the record's first-occurrence index as read (possibly stale-high: it only
+// ever decreases, so it is safe to use to skip an atomicMin).
 template <int KW>
-__device__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h) {
+__device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
+                                                   uint64_t &first_seen) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    constexpr uint32_t KOFF = koff_of(KW);
+    constexpr int NQ = (int)((KOFF + 24 + 15) / 16);   // covers key, tag, ready, first
     const uint64_t tag = h | 1ull;
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     uint64_t s = (h >> 17) & a.mask;
+    first_seen = ~0ull;
     for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
-        uint64_t *slot = a.slots + 2 * s;
-        uint64_t t = ld_agent(slot);
+        const uint32_t off = (uint32_t)(s * a.rec_len);
+        uint32_t d[NQ * 4];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 16 /* sc1 */);
+            d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w;
+        }
+        uint8_t *r = a.rec + off;
+        uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
+        uint32_t ready = d[KOFF / 4 + 2];
         if (t == 0) {
-            uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(slot), 0ull,
-                                     (unsigned long long)tag);
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF), 0ull,
+                                           (unsigned long long)tag);
             if (old == 0) {
-                uint32_t id = atomicAdd(a.counter, 1u);
-                if (id >= a.cap_ids) {
-                    atomicOr(a.err, 1u);
-                    st_agent(slot + 1, (uint64_t)ID_OVF);
-                    return ID_OVF;
-                }
-                uint32_t *dst = a.keys + (uint64_t)id * a.key_stride_w;
 #pragma unroll
                 for (int w = 0; w < KW; w += 2) {
                     if (w + 1 < KW)
-                        st_agent(reinterpret_cast<uint64_t *>(dst + w),
-                                 (uint64_t)k[w] | ((uint64_t)k[w + 1] << 32));
+                        st_agent(reinterpret_cast<uint64_t *>(r + 4 * w), (uint64_t)k[w] | ((uint64_t)k[w + 1] << 32));
                     else
-                        st_agent(dst + w, k[w]);
+                        st_agent(reinterpret_cast<uint32_t *>(r + 4 * w), k[w]);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(slot + 1, (uint64_t)id);
-                return id;
+                st_agent(reinterpret_cast<uint32_t *>(r + KOFF + 8), 1u);
+                return (uint32_t)s;
             }
             t = old;
+            ready = 0;   // the claimer may still be writing the key
         }
         if (t == tag) {
-            uint64_t idv = ld_agent(slot + 1);
-            uint32_t spins = 0;
-            while (idv == (uint64_t)ID_NONE) {
-                __builtin_amdgcn_s_sleep(1);
-                idv = ld_agent(slot + 1);
-                if (++spins > (1u << 22)) {
-                    atomicOr(a.err, 2u);
-                    return ID_OVF;
+            if (!ready) {
+                uint32_t spins = 0;
+                while (ld_agent(reinterpret_cast<const uint32_t *>(r + KOFF + 8)) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) {
+                        atomicOr(a.err, 2u);
+                        return SLOT_OVF;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NQ; ++i) {
+                    const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 16);
+                    d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w;
                 }
             }
-            const uint32_t id = (uint32_t)idv;
-            if (id == ID_OVF) return ID_OVF;
-            const uint32_t *src = a.keys + (uint64_t)id * a.key_stride_w;
             bool eq = true;
 #pragma unroll
-            for (int w = 0; w < KW; w += 2) {
-                if (w + 1 < KW) {
-                    uint64_t v = ld_agent(reinterpret_cast<const uint64_t *>(src + w));
-                    eq = eq && ((uint32_t)v == k[w]) && ((uint32_t)(v >> 32) == k[w + 1]);
-                } else {
-                    eq = eq && (ld_agent(src + w) == k[w]);
-                }
+            for (int w = 0; w < KW; ++w) eq = eq && (d[w] == k[w]);
+            if (eq) {
+                first_seen = (uint64_t)d[KOFF / 4 + 4] | ((uint64_t)d[KOFF / 4 + 5] << 32);
+                return (uint32_t)s;
             }
-            if (eq) return id;
         }
         s = (s + 1) & a.mask;
     }
     atomicOr(a.err, 4u);
-    return ID_OVF;
+    return SLOT_OVF;
 }
 
 template <int KW>
-__global__ __launch_bounds__(TB) void k_groupby(GbArgs a, DevPreds dp) {
+struct LdsCache {
+    static constexpr int KP = (KW + 3) & ~3;   // key words padded to 16 B
+    uint32_t *st;      // E: ST_EMPTY, ST_BUSY or the HBM slot
+    uint64_t *tag;     // E
+    uint32_t *key;     // E x KP
+    uint64_t *agg;     // naggs x E
+    uint64_t *first;   // E
+    uint32_t E;
+};
+
+template <int KW>
+__device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, const uint32_t (&k)[KW]) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(c.key + (uint64_t)e * LdsCache<KW>::KP);
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < LdsCache<KW>::KP / 4; ++q) {
+        const uint4 v = p[q];
+        if (4 * q + 0 < KW) eq = eq && v.x == k[4 * q + 0];
+        if (4 * q + 1 < KW) eq = eq && v.y == k[4 * q + 1];
+        if (4 * q + 2 < KW) eq = eq && v.z == k[4 * q + 2];
+        if (4 * q + 3 < KW) eq = eq && v.w == k[4 * q + 3];
+    }
+    return eq;
+}
+
+// ---- per-row pieces ------------------------------------------------------------------
+// Loads every input byte of the row (all in flight together), applies the predicates and
+// produces the aggregate contributions.  Loads guarded only by uniform count checks leave
+// their register undefined on the other arm, so no copy -- and no wait -- is needed at the
+// join.
+template <class L>
+__device__ __forceinline__ bool load_row(const GbArgs &a, uint64_t row, uint32_t (&k)[L::KW], uint64_t (&v)[AMAX]) {
+    const uint32_t vb = a.valid ? (ldw(a.valid, row) & 0xFFu) : 1u;
+    uint64_t pv[PMAX];
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p)
+        if (p < (int)a.npred) pv[p] = ld_val(a.pptr[p], row, a.pwidth[p]);
+    L::load(a, row, k);
+    uint64_t cv[AMAX];
+#pragma unroll
+    for (int x = 0; x < AMAX; ++x) {
+        if (x < (int)a.naggs) {
+            v[x] = ld_val(a.vptr[x], row, a.vwidth[x]);
+            cv[x] = ld_val(a.cptr[x], row, a.cwidth[x]);
+        }
+    }
+    bool ok = vb != 0;
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p)
+        if (p < (int)a.npred) ok = ok && pred_scalar(pv[p], a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p]);
+#pragma unroll
+    for (int x = 0; x < AMAX; ++x) {
+        if (x < (int)a.naggs) {
+            uint64_t val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(v[x], a.vwidth[x]) : v[x]);
+            if (a.hascond[x] && cv[x] != a.cval[x]) val = 0;
+            v[x] = val;
+        } else {
+            v[x] = 0;
+        }
+    }
+    return ok;
+}
+
+template <int KW>
+__device__ __forceinline__ int lds_lookup(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t &gs) {
+    const uint32_t e0 = (uint32_t)(h >> 40) & (c.E - 1);
+    int slot = -1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t e = e0 ^ (uint32_t)j;
+        const uint32_t s = __hip_atomic_load(&c.st[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (slot < 0 && s < ST_BUSY && c.tag[e] == h && lds_key_eq<KW>(c, e, k)) {
+            slot = (int)e;
+            gs = s;
+        }
+    }
+    return slot;
+}
+
+// adopt an empty LDS entry for a key just resolved in HBM (first come, never evicted)
+template <int KW>
+__device__ __forceinline__ int lds_adopt(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t gs) {
+    const uint32_t e0 = (uint32_t)(h >> 40) & (c.E - 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t e = e0 ^ (uint32_t)j;
+        if (c.st[e] == ST_EMPTY) {
+            if (atomicCAS(&c.st[e], ST_EMPTY, ST_BUSY) == ST_EMPTY) {
+                c.tag[e] = h;
+                uint32_t *kp = c.key + (uint64_t)e * LdsCache<KW>::KP;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) kp[w] = k[w];
+                __hip_atomic_store(&c.st[e], gs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return (int)e;
+            }
+            return -1;   // one attempt only: a lost race falls back to HBM atomics
+        }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ uint64_t *rec_first(const GbArgs &a, uint32_t gs, uint32_t koff) {
+    return reinterpret_cast<uint64_t *>(a.rec + (uint64_t)gs * a.rec_len + koff + 16);
+}
+__device__ __forceinline__ uint64_t *rec_agg(const GbArgs &a, uint32_t gs, uint32_t koff, int x) {
+    return reinterpret_cast<uint64_t *>(a.rec + (uint64_t)gs * a.rec_len + koff + 24 + 8 * x);
+}
+
+template <int KW>
+__device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &c, int slot, uint32_t gs,
+                                           const uint64_t (&v)[AMAX], uint64_t gidx, uint64_t first_seen) {
+    if (slot >= 0) {
+#pragma unroll
+        for (int x = 0; x < AMAX; ++x)
+            if (x < (int)a.naggs && v[x])
+                atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
+        atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
+    } else if (!(a.dbg & 4u)) {
+        constexpr uint32_t KOFF = koff_of(KW);
+#pragma unroll
+        for (int x = 0; x < AMAX; ++x)
+            if (x < (int)a.naggs && v[x])
+                atomicAdd(reinterpret_cast<unsigned long long *>(rec_agg(a, gs, KOFF, x)), (unsigned long long)v[x]);
+        if (first_seen > gidx)
+            atomicMin(reinterpret_cast<unsigned long long *>(rec_first(a, gs, KOFF)), (unsigned long long)gidx);
+    }
+}
+
+// resolve `cnt` queued misses of this wave against the HBM table, one per lane
+template <class L>
+__device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::KW> &c, const uint32_t *q,
+                                             uint32_t qhead, uint32_t cnt, uint32_t lane) {
+    constexpr int KW = L::KW;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < cnt) {
+        const uint64_t row = q[(qhead + lane) % QCAP];
+        uint32_t k[KW];
+        uint64_t v[AMAX];
+        (void)load_row<L>(a, row, k, v);      // predicates already passed
+        const uint64_t h = hash_key<KW>(k);
+        uint32_t gs = SLOT_OVF;
+        uint64_t first_seen = ~0ull;
+        int slot = lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
+        if (slot < 0) {
+            gs = find_or_insert<KW>(a, k, h, first_seen);
+            if (gs != SLOT_OVF) slot = lds_adopt<KW>(c, k, h, gs);
+        }
+        if (gs != SLOT_OVF) accumulate<KW>(a, c, slot, gs, v, a.base_idx + row, first_seen);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <class L>
+__global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
+    constexpr int KW = L::KW;
     extern __shared__ uint64_t lds[];
-    const uint32_t L = a.lds_entries;
-    uint64_t *lfirst = lds;                                   // L
-    uint64_t *lagg = lds + L;                                 // naggs x L
-    uint32_t *ltag = reinterpret_cast<uint32_t *>(lds + L * (1 + a.naggs));   // L
-    for (uint32_t e = threadIdx.x; e < L; e += TB) {
-        ltag[e] = ID_NONE;
-        lfirst[e] = ~0ull;
-        for (uint32_t x = 0; x < a.naggs; ++x) lagg[x * L + e] = 0;
+    LdsCache<KW> c;
+    c.E = a.lds_entries;
+    const uint32_t E = c.E;
+    c.tag = lds;
+    c.first = lds + E;
+    c.agg = lds + 2 * E;
+    c.key = reinterpret_cast<uint32_t *>(lds + (2 + a.naggs) * E);
+    c.st = c.key + (uint64_t)E * LdsCache<KW>::KP;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *q = c.st + E + wave * QCAP;
+    for (uint32_t e = threadIdx.x; e < E; e += GTB) {
+        c.st[e] = ST_EMPTY;
+        c.first[e] = ~0ull;
+        for (uint32_t x = 0; x < a.naggs; ++x) c.agg[x * E + e] = 0;
     }
     __syncthreads();
 
-    const uint64_t stride = (uint64_t)gridDim.x * TB;
-    for (uint64_t row = (uint64_t)blockIdx.x * TB + threadIdx.x; row < a.n; row += stride) {
-        bool ok = true;
-        if (a.valid) ok = a.valid[row] != 0;
-        if (ok && dp.n) ok = preds_match_all(dp, row);
-        if (!ok) continue;
-        uint32_t k[KW];
-        load_key<KW>(a, row, k);
-        const uint64_t h = hash_key<KW>(k);
-        const uint32_t id = find_or_insert<KW>(a, k, h);
-        if (id == ID_OVF) continue;
-        const uint64_t gidx = a.base_idx + row;
-        uint64_t v[AMAX];
-#pragma unroll
-        for (int x = 0; x < AMAX; ++x) {
-            v[x] = 0;
-            if (x < (int)a.naggs) {
-                bool c = true;
-                if (a.cptr[x]) c = ld_scalar(a.cptr[x], a.cwidth[x], row, false) == a.cval[x];
-                if (c) v[x] = a.vcount[x] ? 1ull : ld_scalar(a.vptr[x], a.vwidth[x], row, a.vsign[x] != 0);
+    uint32_t qhead = 0, qn = 0;   // wave-uniform
+    const uint64_t stride = (uint64_t)gridDim.x * GTB;
+    for (uint64_t base = (uint64_t)blockIdx.x * GTB + wave * 64; base < a.n; base += stride) {
+        const uint64_t row = base + lane;
+        bool miss = false;
+        if (row < a.n) {
+            uint32_t k[KW];
+            uint64_t v[AMAX];
+            const bool ok = load_row<L>(a, row, k, v);
+            const uint64_t h = hash_key<KW>(k);
+            if (a.dbg & 1u) {
+                if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live
+            } else if (ok) {
+                uint32_t gs = SLOT_OVF;
+                const int slot = lds_lookup<KW>(c, k, h, gs);
+                if (a.dbg & 8u) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
+                if (slot >= 0) accumulate<KW>(a, c, slot, gs, v, a.base_idx + row, 0);
+                else miss = !(a.dbg & 2u);
             }
         }
-        const uint32_t e = id & (L - 1);
-        uint32_t cur = ltag[e];
-        if (cur == ID_NONE) {
-            cur = atomicCAS(&ltag[e], ID_NONE, id);
-            if (cur == ID_NONE) cur = id;
+        const uint64_t m = __ballot(miss);
+        if (miss) q[(qhead + qn + __popcll(m & lanemask_lt())) % QCAP] = (uint32_t)row;
+        qn += (uint32_t)__popcll(m);
+        if (qn >= 64) {
+            drain_misses<L>(a, c, q, qhead, 64, lane);
+            qhead = (qhead + 64) % QCAP;
+            qn -= 64;
         }
-        if (cur == id) {
+    }
+    while (qn) {
+        const uint32_t cnt = qn < 64 ? qn : 64;
+        drain_misses<L>(a, c, q, qhead, cnt, lane);
+        qhead = (qhead + cnt) % QCAP;
+        qn -= cnt;
+    }
+
+    __syncthreads();
+    constexpr uint32_t KOFF = koff_of(KW);
+    for (uint32_t e = threadIdx.x; e < E; e += GTB) {
+        const uint32_t gs = c.st[e];
+        if (gs >= ST_BUSY) continue;
+        for (uint32_t x = 0; x < a.naggs; ++x) {
+            const uint64_t s = c.agg[x * E + e];
+            if (s) atomicAdd(reinterpret_cast<unsigned long long *>(rec_agg(a, gs, KOFF, (int)x)), (unsigned long long)s);
+        }
+        const uint64_t f = c.first[e];
+        if (ld_agent(rec_first(a, gs, KOFF)) > f)
+            atomicMin(reinterpret_cast<unsigned long long *>(rec_first(a, gs, KOFF)), (unsigned long long)f);
+    }
+}
+
+// per-interval reset: tag/ready = 0, first = ~0, aggregates = 0 (keys are left as is)
+__global__ void k_table_reset(uint8_t *rec, uint32_t rec_len, uint32_t koff, uint32_t naggs, uint64_t ns,
+                              uint32_t *err) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+        uint64_t *h = reinterpret_cast<uint64_t *>(rec + i * rec_len + koff);
+        h[0] = 0;
+        h[1] = 0;
+        h[2] = ~0ull;
+        for (uint32_t x = 0; x < naggs; ++x) h[3 + x] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;
+}
+
+// ---- finalize: list the occupied slots in ascending order ----------------------------
+constexpr int CT = 1024;   // slots per compaction tile (256 threads x 4)
+
+__global__ __launch_bounds__(256) void k_slots_count(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff,
+                                                     uint64_t ns, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t wc[4];
+    uint32_t c = 0;
 #pragma unroll
-            for (int x = 0; x < AMAX; ++x)
-                if (x < (int)a.naggs && v[x])
-                    atomicAdd(reinterpret_cast<unsigned long long *>(&lagg[x * L + e]),
-                              (unsigned long long)v[x]);
-            atomicMin(reinterpret_cast<unsigned long long *>(&lfirst[e]), (unsigned long long)gidx);
-        } else {
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
+        const bool occ = s < ns && *reinterpret_cast<const uint64_t *>(rec + s * rec_len + koff) != 0;
+        c += __popcll(__ballot(occ));
+    }
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, uint64_t m, uint64_t *__restrict__ total) {
+    __shared__ uint32_t part[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t b = threadIdx.x * per, e = min(m, b + per);
+    uint32_t s = 0;
+    for (uint64_t i = b; i < e; ++i) s += v[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        uint32_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (uint64_t i = b; i < e; ++i) {
+        uint32_t c = v[i];
+        v[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_slots_write(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff,
+                                                     uint64_t ns, const uint32_t *__restrict__ off,
+                                                     uint32_t *__restrict__ out) {
+    __shared__ uint32_t wpre[16];
+    __shared__ uint64_t wmask[16];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-            for (int x = 0; x < AMAX; ++x)
-                if (x < (int)a.naggs && v[x])
-                    atomicAdd(reinterpret_cast<unsigned long long *>(&a.aggs[x][id]),
-                              (unsigned long long)v[x]);
-            if (ld_agent(&a.first[id]) > gidx)
-                atomicMin(reinterpret_cast<unsigned long long *>(&a.first[id]), (unsigned long long)gidx);
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
+        const bool occ = s < ns && *reinterpret_cast<const uint64_t *>(rec + s * rec_len + koff) != 0;
+        const uint64_t m = __ballot(occ);
+        if (lane == 0) wmask[j * 4 + wave] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = 0;
+        for (int w = 0; w < 16; ++w) {
+            wpre[w] = r;
+            r += __popcll(wmask[w]);
         }
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < L; e += TB) {
-        const uint32_t id = ltag[e];
-        if (id == ID_NONE) continue;
-        for (uint32_t x = 0; x < a.naggs; ++x) {
-            const uint64_t s = lagg[x * L + e];
-            if (s) atomicAdd(reinterpret_cast<unsigned long long *>(&a.aggs[x][id]), (unsigned long long)s);
+    const uint32_t base = off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t w = j * 4 + wave;
+        const uint64_t m = wmask[w];
+        if ((m >> lane) & 1ull) {
+            const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
+            out[base + wpre[w] + __popcll(m & lanemask_lt())] = (uint32_t)s;
         }
-        const uint64_t f = lfirst[e];
-        if (ld_agent(&a.first[id]) > f)
-            atomicMin(reinterpret_cast<unsigned long long *>(&a.first[id]), (unsigned long long)f);
     }
 }
 
-__global__ void k_table_reset(uint64_t *slots, uint64_t nslots, uint64_t *first, uint64_t nfirst,
-                              uint64_t **aggs, uint32_t naggs, uint32_t *counter) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride) {
-        slots[2 * i] = 0;
-        slots[2 * i + 1] = ID_NONE;
-    }
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nfirst; i += stride) {
-        first[i] = ~0ull;
-        for (uint32_t x = 0; x < naggs; ++x) aggs[x][i] = 0;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 2) counter[threadIdx.x] = 0;
-}
+// materialise selected groups as packed rows key | aggs | first (the Stats rows of
+// nextStats, tracer.go:186-219); aggregates wrap to their out_width (the BPF value width)
+struct AggMasks {
+    uint32_t m[2 * AMAX];   // (lo, hi) word masks per aggregate
+};
 
-// groups: copy counter -> u64 n_groups (clamped to cap)
-__global__ void k_count(const uint32_t *counter, uint32_t cap, uint64_t *n) {
-    uint32_t c = counter[0];
-    *n = c > cap ? cap : c;
+__global__ void k_gather_rows(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff, uint32_t key_words,
+                              uint32_t naggs, AggMasks am, const uint32_t *__restrict__ idx, uint64_t ns, uint64_t k,
+                              uint8_t *__restrict__ out) {
+    const uint64_t r = blockIdx.x;
+    if (r >= k) return;
+    const uint32_t row_words = key_words + 2 * naggs + 2;
+    uint32_t *o = reinterpret_cast<uint32_t *>(out) + r * row_words;
+    const uint32_t g = idx[r];
+    const bool ok = g < ns;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rec + (uint64_t)g * rec_len);
+    for (uint32_t w = threadIdx.x; w < row_words; w += blockDim.x) {
+        uint32_t v = 0;
+        if (ok) {
+            if (w < key_words) v = src[w];
+            else if (w < key_words + 2 * naggs) v = src[(koff + 24) / 4 + (w - key_words)] & am.m[w - key_words];
+            else v = src[(koff + 16) / 4 + (w - key_words - 2 * naggs)];
+        }
+        o[w] = v;
+    }
 }
 
 }  // namespace
@@ -278,34 +642,66 @@ struct igx_table {
     uint32_t nkeys = 0;
     uint32_t key_widths[32] = {};
     uint32_t key_words = 0;      // packed words (each column padded to 4 B)
-    uint32_t kw_inst = 0;        // instantiated KW >= key_words
-    uint32_t key_stride_w = 0;
+    uint32_t kw_rec = 0;         // key words as the kernel lays them out (static KW or generic width)
+    uint32_t koff = 0, rec_len = 0;
+    bool generic = false;        // no compile-time layout (or IGX_GB_GENERIC at create)
     igx_agg aggs[AMAX] = {};
     uint32_t naggs = 0;
-    uint64_t cap = 0;            // dense ids
+    uint64_t cap = 0;            // distinct keys promised by the caller
     uint64_t nslots = 0;
-    uint64_t *slots = nullptr;
-    uint32_t *keys = nullptr;
-    uint64_t *aggv[AMAX] = {};
-    uint64_t **d_aggv = nullptr;
-    uint64_t *first = nullptr;
-    uint32_t *counter = nullptr;  // [0] = ids, [1] = err
+    uint8_t *rec = nullptr;
+    uint32_t *err = nullptr;
+    uint32_t *groups = nullptr;  // occupied slots after finalize
+    uint32_t *tile_cnt = nullptr;
     uint64_t *n_groups = nullptr;
+    uint64_t host_groups = 0;
+    unsigned long long *dbg_cnt = nullptr;
 };
+
+// compile-time key layouts: the reference's BPF key structs + single-column keys
+using TcpKey = StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>;   // ip_key_t (tcptop.h:8-17)
+using FileKey = StaticLayout<8, 4, 4, 4>;                 // file_id (filetop.h:13-18)
+using NetPolicyKey = StaticLayout<4, 1, 4, 2>;            // (src, direction, peer, port)
+
+template <class L>
+static bool layout_is(const uint32_t *widths, uint32_t nkeys) {
+    if constexpr (L::is_static) {
+        if (nkeys != (uint32_t)L::NC) return false;
+        for (int c = 0; c < L::NC; ++c)
+            if ((int)widths[c] != L::Ws[c]) return false;
+        return true;
+    }
+    return false;
+}
 
 static const int kInst[] = {2, 4, 6, 8, 12, 18, 24, 32};
 
-extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys,
-                                  const igx_agg *aggs, uint32_t naggs, uint64_t capacity,
-                                  igx_table **out) {
-    if (!ctx || !out || !key_widths || nkeys == 0 || nkeys > 32)
+// key words the kernel will use for this key description (0 = generic)
+static int static_kw(const uint32_t *w, uint32_t n) {
+    if (std::getenv("IGX_GB_GENERIC")) return 0;   // diagnostics
+    if (layout_is<TcpKey>(w, n)) return TcpKey::KW;
+    if (layout_is<FileKey>(w, n)) return FileKey::KW;
+    if (layout_is<NetPolicyKey>(w, n)) return NetPolicyKey::KW;
+    if (n == 1 && (w[0] == 1 || w[0] == 2 || w[0] == 4 || w[0] == 8 || w[0] == 16)) return (int)((w[0] + 3) / 4);
+    return 0;
+}
+
+extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys, const igx_agg *aggs,
+                                  uint32_t naggs, uint64_t capacity, igx_table **out) {
+    if (!ctx || !out || !key_widths || nkeys == 0 || nkeys > 16)
         return igx_fail(ctx, IGX_EINVAL, "groupby_create: bad key description");
     if (naggs > AMAX) return igx_fail(ctx, IGX_ENOTSUP, "groupby_create: more than %d aggregates", AMAX);
-    if (capacity == 0 || capacity >= 0xFFFFFFF0ull)
-        return igx_fail(ctx, IGX_EINVAL, "groupby_create: bad capacity");
+    for (uint32_t x = 0; x < naggs; ++x) {
+        const uint32_t ow = aggs[x].out_width;
+        if (ow != 0 && ow != 1 && ow != 2 && ow != 4 && ow != 8)
+            return igx_fail(ctx, IGX_EINVAL, "groupby_create: aggregate %u out_width %u", x, ow);
+        if (aggs[x].kind != IGX_AGG_COUNT && aggs[x].kind != IGX_AGG_SUM)
+            return igx_fail(ctx, IGX_EINVAL, "groupby_create: aggregate %u kind %u", x, aggs[x].kind);
+    }
+    if (capacity == 0 || capacity > (1ull << 28)) return igx_fail(ctx, IGX_EINVAL, "groupby_create: bad capacity");
     uint32_t words = 0;
     for (uint32_t i = 0; i < nkeys; ++i) {
-        uint32_t w = key_widths[i];
+        const uint32_t w = key_widths[i];
         if (w == 0 || w == 3 || (w > 4 && w % 4)) return igx_fail(ctx, IGX_ENOTSUP, "groupby: key width %u", w);
         words += (w + 3) / 4;
     }
@@ -315,24 +711,40 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     t->nkeys = nkeys;
     for (uint32_t i = 0; i < nkeys; ++i) t->key_widths[i] = key_widths[i];
     t->key_words = words;
-    for (int k : kInst)
-        if ((uint32_t)k >= words) { t->kw_inst = k; break; }
-    t->key_stride_w = (uint32_t)igx_align(t->kw_inst, 4);   // 16-B aligned keys
+    const int skw = static_kw(key_widths, nkeys);
+    t->generic = skw == 0;
+    if (skw) {
+        t->kw_rec = (uint32_t)skw;
+    } else {
+        for (int k : kInst)
+            if ((uint32_t)k >= words) {
+                t->kw_rec = (uint32_t)k;
+                break;
+            }
+    }
+    t->koff = koff_of((int)t->kw_rec);
+    t->rec_len = rec_bytes((int)t->kw_rec, naggs);
     t->naggs = naggs;
     for (uint32_t i = 0; i < naggs; ++i) t->aggs[i] = aggs[i];
     t->cap = capacity;
     uint64_t ns = 1024;
     while (ns < 2 * capacity) ns <<= 1;
     t->nslots = ns;
-    hipError_t e = hipMalloc(&t->slots, ns * 16);
-    if (e == hipSuccess) e = hipMalloc(&t->keys, capacity * t->key_stride_w * 4);
-    for (uint32_t i = 0; i < naggs && e == hipSuccess; ++i) e = hipMalloc(&t->aggv[i], capacity * 8);
-    if (e == hipSuccess) e = hipMalloc(&t->d_aggv, AMAX * sizeof(uint64_t *));
-    if (e == hipSuccess) e = hipMalloc(&t->first, capacity * 8);
-    if (e == hipSuccess) e = hipMalloc(&t->counter, 64);
+    if (ns * t->rec_len >= (1ull << 32)) {
+        const uint32_t r = t->rec_len;
+        delete t;
+        return igx_fail(ctx, IGX_ENOTSUP, "groupby_create: table of %llu x %u B exceeds 4 GiB",
+                        (unsigned long long)ns, r);
+    }
+    const uint64_t tiles = (ns + CT - 1) / CT;
+    hipError_t e = hipMalloc(&t->rec, ns * t->rec_len);
+    if (e == hipSuccess) e = hipMemsetAsync(t->rec, 0, ns * t->rec_len, ctx->stream);
+    if (e == hipSuccess) e = hipMalloc(&t->err, 64);
+    if (e == hipSuccess) e = hipMalloc(&t->groups, ns * 4);
+    if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
     if (e == hipSuccess) e = hipMalloc(&t->n_groups, 64);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(t->d_aggv, t->aggv, AMAX * sizeof(uint64_t *), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
+    if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream);
     if (e != hipSuccess) {
         igx_groupby_destroy(t);
         return igx_fail(ctx, IGX_ENOMEM, "groupby_create: %s", hipGetErrorString(e));
@@ -344,71 +756,86 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
 extern "C" int igx_groupby_reset(igx_table *t) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    hipLaunchKernelGGL(k_table_reset, dim3(1024), dim3(256), 0, ctx->stream, t->slots, t->nslots,
-                       t->first, t->cap, t->d_aggv, t->naggs, t->counter);
+    hipLaunchKernelGGL(k_table_reset, dim3(2048), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff, t->naggs,
+                       t->nslots, t->err);
     IGX_HIP(ctx, hipGetLastError());
+    t->host_groups = 0;
     return IGX_OK;
 }
 
 extern "C" int igx_groupby_destroy(igx_table *t) {
     if (!t) return IGX_OK;
     (void)hipStreamSynchronize(t->ctx->stream);
-    (void)hipFree(t->slots);
-    (void)hipFree(t->keys);
-    for (auto *p : t->aggv) (void)hipFree(p);
-    (void)hipFree(t->d_aggv);
-    (void)hipFree(t->first);
-    (void)hipFree(t->counter);
+    (void)hipFree(t->rec);
+    (void)hipFree(t->err);
+    (void)hipFree(t->groups);
+    (void)hipFree(t->tile_cnt);
     (void)hipFree(t->n_groups);
+    (void)hipFree(t->dbg_cnt);
     delete t;
     return IGX_OK;
 }
 
-template <int KW>
-static void launch_gb(igx_ctx *ctx, const GbArgs &a, const DevPreds &dp, uint32_t blocks, size_t lds) {
-    hipLaunchKernelGGL(k_groupby<KW>, dim3(blocks), dim3(TB), lds, ctx->stream, a, dp);
+constexpr size_t GB_LDS_BUDGET = 120 * 1024;   // cache; + 8 KB of miss queues
+
+template <class L>
+static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BUDGET + 8192);
+        attr = true;
+    }
+    const size_t entry = 4 + 8 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
+    uint32_t E = 8192;
+    while (E > 64 && E * entry > GB_LDS_BUDGET) E >>= 1;
+    a.lds_entries = E;
+    hipLaunchKernelGGL(k_groupby<L>, dim3(blocks), dim3(GTB), E * entry + (GTB / 64) * QCAP * 4, ctx->stream, a);
 }
 
-extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols,
-                                  const uint32_t *key_cols, const igx_pred *preds, uint32_t npreds,
-                                  uint64_t nrows, uint64_t base_idx) {
+extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
+                                  const igx_pred *preds, uint32_t npreds, uint64_t nrows, uint64_t base_idx) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     if (nrows == 0) return IGX_OK;
     if (!cols || !key_cols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: null columns");
+    if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "groupby_update: more than 2^32 rows in one call");
     GbArgs a{};
-    // key words
     uint32_t w = 0;
     for (uint32_t k = 0; k < t->nkeys; ++k) {
-        uint32_t ci = key_cols[k];
+        const uint32_t ci = key_cols[k];
         if (ci >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: key column %u out of range", ci);
         const igx_col &c = cols[ci];
         if (c.width != t->key_widths[k])
             return igx_fail(ctx, IGX_EINVAL, "groupby_update: key column %u width %u != %u", k, c.width,
                             t->key_widths[k]);
         const uint8_t *p = static_cast<const uint8_t *>(c.ptr);
+        const uintptr_t need = c.width >= 16 ? 16 : (c.width >= 4 ? 4 : c.width);
+        if (reinterpret_cast<uintptr_t>(p) & (need - 1))
+            return igx_fail(ctx, IGX_EINVAL, "groupby_update: key column %u misaligned", k);
+        a.kcol[k] = p;
         const uint32_t nw = (c.width + 3) / 4;
-        const bool x4 = (c.width % 16 == 0) && ((reinterpret_cast<uintptr_t>(p) & 15) == 0);
         for (uint32_t j = 0; j < nw; ++j, ++w) {
             a.kptr[w] = p;
             a.kwidth[w] = c.width;
             a.koff[w] = 4 * j;
-            if (c.width == 1) a.kmode[w] = KM_U8;
-            else if (c.width == 2) a.kmode[w] = KM_U16;
-            else if (x4) a.kmode[w] = (j % 4 == 0) ? KM_X4 : KM_CONT;
-            else a.kmode[w] = KM_U32;
+            a.kmask[w] = c.width >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c.width)) - 1u);
         }
     }
-    for (; w < KWMAX; ++w) a.kmode[w] = KM_ZERO;
-    // x4 groups must fit inside the instantiated width
-    for (uint32_t q = 0; q < (uint32_t)t->kw_inst; ++q)
-        if (a.kmode[q] == KM_X4 && q + 3 >= (uint32_t)t->kw_inst)
-            for (uint32_t r = q; r < (uint32_t)t->kw_inst; ++r) a.kmode[r] = KM_U32;
-    // aggregates
+    // any readable dword for loads whose result is discarded (padding words, COUNT, no cond)
+    const uint8_t *dummy = static_cast<const uint8_t *>(cols[key_cols[0]].ptr);
+    for (; w < KWMAX; ++w) {
+        a.kptr[w] = dummy;
+        a.kwidth[w] = 0;
+        a.koff[w] = 0;
+        a.kmask[w] = 0;
+    }
     a.naggs = t->naggs;
     for (uint32_t x = 0; x < t->naggs; ++x) {
         const igx_agg &g = t->aggs[x];
         a.vcount[x] = g.kind == IGX_AGG_COUNT;
+        a.vptr[x] = dummy;
+        a.vwidth[x] = 1;
         if (!a.vcount[x]) {
             if (g.col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: agg column out of range");
             a.vptr[x] = static_cast<const uint8_t *>(cols[g.col].ptr);
@@ -419,46 +846,75 @@ extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t nc
             if (cols[g.col].kind == IGX_KIND_FLOAT)
                 return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: float sums are not supported");
         }
+        a.cptr[x] = dummy;
+        a.cwidth[x] = 1;
         if (g.cond_col != IGX_NO_COL) {
             if (g.cond_col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: cond column out of range");
+            const uint32_t cw = cols[g.cond_col].width;
+            if (cw != 1 && cw != 2 && cw != 4 && cw != 8)
+                return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: condition width %u", cw);
             a.cptr[x] = static_cast<const uint8_t *>(cols[g.cond_col].ptr);
-            a.cwidth[x] = cols[g.cond_col].width;
-            a.cval[x] = g.cond_val;
+            a.cwidth[x] = cw;
+            a.cval[x] = cw == 8 ? g.cond_val : (g.cond_val & ((1ull << (8 * cw)) - 1));
+            a.hascond[x] = 1;
         }
-        a.aggs[x] = t->aggv[x];
     }
-    DevPreds dp{};
-    int rc = igx_build_preds(ctx, cols, ncols, preds, npreds, &dp);
-    if (rc) return rc;
+    if (npreds > PMAX) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: more than %d predicates", PMAX);
+    for (uint32_t p = 0; p < npreds; ++p) {
+        const igx_pred &q = preds[p];
+        if (q.col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: predicate column out of range");
+        const igx_col &c = cols[q.col];
+        if (q.cmp == IGX_CMP_REGEX || c.kind == IGX_KIND_BYTES || c.kind == IGX_KIND_BOOL ||
+            c.kind == IGX_KIND_OTHER || (c.width != 1 && c.width != 2 && c.width != 4 && c.width != 8) ||
+            (c.kind == IGX_KIND_FLOAT && c.width < 4))
+            return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: predicate %u is not a scalar comparison "
+                                              "(run igx_filter first)", p);
+        a.pptr[p] = static_cast<const uint8_t *>(c.ptr);
+        a.pwidth[p] = c.width;
+        a.pkind[p] = c.kind;
+        a.pcmp[p] = q.cmp;
+        a.pneg[p] = q.negate;
+        uint64_t r = 0;
+        for (uint32_t b = 0; b < c.width; ++b) r |= (uint64_t)q.ref[b] << (8 * b);
+        a.pref[p] = r;
+    }
+    a.npred = npreds;
     a.valid = nullptr;
     a.n = nrows;
     a.base_idx = base_idx;
-    a.slots = t->slots;
-    a.keys = t->keys;
-    a.key_stride_w = t->key_stride_w;
-    a.first = t->first;
-    a.counter = t->counter;
-    a.err = t->counter + 1;
+    a.rec = t->rec;
+    a.rec_len = t->rec_len;
+    a.rec_total = (uint32_t)(t->nslots * t->rec_len);
+    a.err = t->err;
     a.mask = t->nslots - 1;
-    a.cap_ids = (uint32_t)t->cap;
     a.max_probe = (uint32_t)std::min<uint64_t>(t->nslots, 1u << 20);
-    // LDS staging: L entries x (8 first + 8 naggs + 4 tag) bytes, <= 48 KB
-    uint32_t L = 2048;
-    while (L > 64 && (size_t)L * (12 + 8 * t->naggs) > 48 * 1024) L >>= 1;
-    a.lds_entries = L;
-    const size_t lds = (size_t)L * (12 + 8 * t->naggs);
-    const uint64_t want = (nrows + TB - 1) / TB;
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus * 3));
-    switch (t->kw_inst) {
-    case 2: launch_gb<2>(ctx, a, dp, blocks, lds); break;
-    case 4: launch_gb<4>(ctx, a, dp, blocks, lds); break;
-    case 6: launch_gb<6>(ctx, a, dp, blocks, lds); break;
-    case 8: launch_gb<8>(ctx, a, dp, blocks, lds); break;
-    case 12: launch_gb<12>(ctx, a, dp, blocks, lds); break;
-    case 18: launch_gb<18>(ctx, a, dp, blocks, lds); break;
-    case 24: launch_gb<24>(ctx, a, dp, blocks, lds); break;
-    default: launch_gb<32>(ctx, a, dp, blocks, lds); break;
-    }
+    if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
+    a.dbg_cnt = t->dbg_cnt;
+    const uint64_t want = (nrows + GTB - 1) / GTB;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus));
+    const uint32_t *kw = t->key_widths;
+    if (t->generic) {
+        switch (t->kw_rec) {
+        case 2: launch_gb<GenericLayout<2>>(ctx, a, blocks); break;
+        case 4: launch_gb<GenericLayout<4>>(ctx, a, blocks); break;
+        case 6: launch_gb<GenericLayout<6>>(ctx, a, blocks); break;
+        case 8: launch_gb<GenericLayout<8>>(ctx, a, blocks); break;
+        case 12: launch_gb<GenericLayout<12>>(ctx, a, blocks); break;
+        case 18: launch_gb<GenericLayout<18>>(ctx, a, blocks); break;
+        case 24: launch_gb<GenericLayout<24>>(ctx, a, blocks); break;
+        case 32: launch_gb<GenericLayout<32>>(ctx, a, blocks); break;
+        default: return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: no kernel for %u key words", t->kw_rec);
+        }
+    } else if (layout_is<TcpKey>(kw, t->nkeys)) launch_gb<TcpKey>(ctx, a, blocks);
+    else if (layout_is<FileKey>(kw, t->nkeys)) launch_gb<FileKey>(ctx, a, blocks);
+    else if (layout_is<NetPolicyKey>(kw, t->nkeys))
+        launch_gb<NetPolicyKey>(ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 1) launch_gb<StaticLayout<1>>(ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 2) launch_gb<StaticLayout<2>>(ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 4) launch_gb<StaticLayout<4>>(ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 8) launch_gb<StaticLayout<8>>(ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 16) launch_gb<StaticLayout<16>>(ctx, a, blocks);
+    else return igx_fail(ctx, IGX_EINVAL, "groupby_update: internal layout mismatch");
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }
@@ -466,71 +922,103 @@ extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t nc
 extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    hipLaunchKernelGGL(k_count, dim3(1), dim3(1), 0, ctx->stream, t->counter, (uint32_t)t->cap, t->n_groups);
+    const uint64_t tiles = (t->nslots + CT - 1) / CT;
+    hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff,
+                       t->nslots, t->tile_cnt);
+    hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups);
+    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff,
+                       t->nslots, t->tile_cnt, t->groups);
+    IGX_HIP(ctx, hipGetLastError());
     uint64_t *h;
     int rc = igx_pinned(ctx, 16, reinterpret_cast<void **>(&h));
     if (rc) return rc;
     IGX_HIP(ctx, hipMemcpyAsync(h, t->n_groups, 8, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipMemcpyAsync(reinterpret_cast<uint32_t *>(h) + 2, t->counter + 1, 4,
-                                hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(reinterpret_cast<uint32_t *>(h) + 2, t->err, 4, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t ng = h[0];
     const uint32_t err = reinterpret_cast<uint32_t *>(h)[2];
+    t->host_groups = ng;
     if (view) {
         view->n_groups = ng;
+        view->n_slots = t->nslots;
         view->key_bytes = t->key_words * 4;
-        view->key_stride = t->key_stride_w * 4;
+        view->key_stride = t->rec_len;
         view->naggs = t->naggs;
-        view->keys = reinterpret_cast<const uint8_t *>(t->keys);
-        for (uint32_t x = 0; x < 16; ++x) view->aggs[x] = x < t->naggs ? t->aggv[x] : nullptr;
-        view->first_idx = t->first;
+        view->keys = t->rec;
+        for (uint32_t x = 0; x < 16; ++x)
+            view->aggs[x] = x < t->naggs ? reinterpret_cast<const uint64_t *>(t->rec + t->koff + 24 + 8 * x) : nullptr;
+        view->first_idx = reinterpret_cast<const uint64_t *>(t->rec + t->koff + 16);
+        view->groups = t->groups;
         view->d_n_groups = t->n_groups;
     }
-    if (err & 1) return igx_fail(ctx, IGX_ENOSPC, "groupby: more than %llu distinct keys", (unsigned long long)t->cap);
-    if (err) return igx_fail(ctx, IGX_EIO, "groupby: table probe failure (err=%u)", err);
+    if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
+    if (ng > t->cap)
+        return igx_fail(ctx, IGX_ENOSPC, "groupby: %llu distinct keys exceed capacity %llu",
+                        (unsigned long long)ng, (unsigned long long)t->cap);
     return IGX_OK;
 }
-
-// ---------------------------------------------------------------------------------------
-// materialise selected groups (the Stats rows of nextStats, tracer.go:186-219)
-// ---------------------------------------------------------------------------------------
-namespace {
-__global__ void k_gather_rows(const uint32_t *__restrict__ keys, uint32_t key_stride_w, uint32_t key_words,
-                              const uint64_t *const *__restrict__ aggs, uint32_t naggs,
-                              const uint64_t *__restrict__ first, const uint32_t *__restrict__ idx,
-                              const uint64_t *__restrict__ n_groups, uint64_t k, uint8_t *__restrict__ out) {
-    const uint64_t r = blockIdx.x;
-    if (r >= k) return;
-    const uint32_t row_words = key_words + 2 * naggs + 2;
-    uint32_t *o = reinterpret_cast<uint32_t *>(out) + r * row_words;
-    const uint32_t g = idx[r];
-    const bool ok = g < *n_groups;
-    for (uint32_t w = threadIdx.x; w < row_words; w += blockDim.x) {
-        uint32_t v = 0;
-        if (ok) {
-            if (w < key_words) v = keys[(uint64_t)g * key_stride_w + w];
-            else if (w < key_words + 2 * naggs) {
-                const uint32_t a = (w - key_words) >> 1;
-                const uint64_t s = aggs[a][g];
-                v = ((w - key_words) & 1) ? (uint32_t)(s >> 32) : (uint32_t)s;
-            } else {
-                const uint64_t f = first[g];
-                v = ((w - key_words - 2 * naggs) & 1) ? (uint32_t)(f >> 32) : (uint32_t)f;
-            }
-        }
-        o[w] = v;
-    }
-}
-}  // namespace
 
 extern "C" int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     if (k == 0) return IGX_OK;
     if (!idx || !out_rows) return igx_fail(ctx, IGX_EINVAL, "groupby_gather: null argument");
-    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)k), dim3(64), 0, ctx->stream, t->keys, t->key_stride_w,
-                       t->key_words, (const uint64_t *const *)t->d_aggv, t->naggs, t->first, idx,
-                       t->n_groups, k, out_rows);
+    AggMasks am{};
+    for (uint32_t x = 0; x < t->naggs; ++x) {
+        const uint32_t ow = t->aggs[x].out_width;
+        const uint64_t m = (ow == 0 || ow >= 8) ? ~0ull : ((1ull << (8 * ow)) - 1);
+        am.m[2 * x] = (uint32_t)m;
+        am.m[2 * x + 1] = (uint32_t)(m >> 32);
+    }
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)k), dim3(64), 0, ctx->stream, t->rec, t->rec_len, t->koff,
+                       t->key_words, t->naggs, am, idx, t->nslots, k, out_rows);
     IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
+
+// Sort / top-K over the table's groups without materialising them (rows are the occupied
+// slots; keys read through the slot list at the record stride).
+extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uint32_t k,
+                                uint32_t *out_slots) {
+    if (!t) return IGX_EINVAL;
+    igx_ctx *ctx = t->ctx;
+    if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "groupby_sort: more than 8 keys");
+    igx_sortkey sk[8];
+    uint32_t strides[8];
+    for (uint32_t i = 0; i < nkeys; ++i) {
+        const igx_tsortkey &q = keys[i];
+        sk[i] = igx_sortkey{};
+        sk[i].desc = q.desc;
+        strides[i] = t->rec_len;
+        if (q.src == IGX_TSRC_AGG) {
+            if (q.index >= t->naggs) return igx_fail(ctx, IGX_EINVAL, "groupby_sort: aggregate %u", q.index);
+            sk[i].ptr = t->rec + t->koff + 24 + 8 * q.index;   // little endian: the low out_width bytes
+            sk[i].width = t->aggs[q.index].out_width ? t->aggs[q.index].out_width : 8;   // are the wrapped value
+            sk[i].kind = IGX_KIND_UINT;
+        } else if (q.src == IGX_TSRC_FIRST) {
+            sk[i].ptr = t->rec + t->koff + 16;
+            sk[i].width = 8;
+            sk[i].kind = IGX_KIND_UINT;
+        } else if (q.src == IGX_TSRC_KEY) {
+            if (q.offset + q.width > t->key_words * 4)
+                return igx_fail(ctx, IGX_EINVAL, "groupby_sort: key bytes out of range");
+            sk[i].ptr = t->rec + q.offset;
+            sk[i].width = q.width;
+            sk[i].kind = q.kind;
+        } else {
+            return igx_fail(ctx, IGX_EINVAL, "groupby_sort: bad source");
+        }
+    }
+    return sort_common_rows(ctx, sk, strides, nkeys, t->host_groups, t->groups,
+                            reinterpret_cast<const uint64_t *>(t->rec + t->koff + 16), t->rec_len, k, out_slots);
+}
+
+// Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.
+extern "C" int igx_groupby_debug_counts(igx_table *t, uint64_t *out4) {
+    if (!t || !out4) return IGX_EINVAL;
+    igx_ctx *ctx = t->ctx;
+    IGX_HIP(ctx, hipMemcpyAsync(out4, t->dbg_cnt, 32, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    IGX_HIP(ctx, hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream));
     return IGX_OK;
 }

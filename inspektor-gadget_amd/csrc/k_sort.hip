@@ -31,10 +31,11 @@ constexpr int MAXW = 80;          // composed words (<= 8 keys x 64-byte strings
 
 struct ComposeArgs {
     const uint8_t *ptr[8];
-    uint32_t width[8], kind[8], desc[8], words[8];
-    uint32_t nkeys, has_nil, pos_words, pos_not;
+    uint32_t width[8], kind[8], desc[8], words[8], rstride[8];
+    uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
     const uint64_t *pos;
     const uint8_t *valid;
+    const uint32_t *rowmap;
     uint64_t n, stride;   // stride = words array pitch (elements)
 };
 
@@ -52,7 +53,8 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
                                                 uint32_t *__restrict__ payload) {
     uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= a.n) return;
-    bool nil = a.valid && a.valid[i] == 0;
+    const uint64_t src = a.rowmap ? a.rowmap[i] : i;   // where row i's values live
+    bool nil = a.valid && a.valid[src] == 0;
     uint32_t w = 0;
     if (a.has_nil) words[(w++) * a.stride + i] = nil ? 1u : 0u;
     for (uint32_t k = 0; k < a.nkeys; ++k) {
@@ -63,17 +65,17 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
             continue;
         }
         const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
+        const uint8_t *p = a.ptr[k] + src * a.rstride[k];
         if (a.kind[k] == IGX_KIND_BYTES) {
-            const uint8_t *p = a.ptr[k] + i * a.width[k];
             for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
             if (a.width[k] == 4) {
-                uint32_t b = reinterpret_cast<const uint32_t *>(a.ptr[k])[i];
+                uint32_t b = *reinterpret_cast<const uint32_t *>(p);
                 if (b == 0x80000000u) b = 0;                       // -0 == +0 in Go
                 b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
                 words[w * a.stride + i] = b ^ inv;
             } else {
-                uint64_t b = reinterpret_cast<const uint64_t *>(a.ptr[k])[i];
+                uint64_t b = *reinterpret_cast<const uint64_t *>(p);
                 if (b == 0x8000000000000000ull) b = 0;
                 b = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
                 words[w * a.stride + i] = (uint32_t)(b >> 32) ^ inv;
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
             }
         } else {
             const bool sgn = a.kind[k] == IGX_KIND_INT;
-            uint64_t v = ld_scalar(a.ptr[k], a.width[k], i, false);
+            uint64_t v = ld_scalar(p, a.width[k], 0, false);
             if (sgn) v ^= 1ull << (8 * a.width[k] - 1);
             if (nw == 1) {
                 words[w * a.stride + i] = (uint32_t)v ^ inv;
@@ -92,7 +94,9 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
         }
         w += nw;
     }
-    uint64_t p = a.pos ? a.pos[i] : i;
+    uint64_t p = a.pos ? *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(a.pos) +
+                                                             src * a.pos_stride)
+                       : i;
     if (a.pos_not && !nil) p = ~p;
     if (a.pos_words == 2) {
         words[w * a.stride + i] = (uint32_t)(p >> 32);
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
     } else {
         words[w * a.stride + i] = (uint32_t)p;
     }
-    payload[i] = (uint32_t)i;
+    payload[i] = (uint32_t)src;
 }
 
 // per-word AND / OR over all rows -> res[2*w] (and), res[2*w+1] (or)
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
 
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
-                     uint32_t *out_perm, uint32_t limit) {
+                     uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride) {
     if (nrows == 0) return IGX_OK;
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
     if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than 8 keys");
@@ -242,8 +246,10 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         ca.kind[k] = keys[k].kind;
         ca.desc[k] = keys[k].desc_eff;
         ca.words[k] = keys[k].words;
+        ca.rstride[k] = keys[k].stride ? keys[k].stride : keys[k].width;
         KW += keys[k].words;
     }
+    ca.rowmap = rowmap;
     const uint32_t pos_words = (pos == nullptr) ? 1 : 2;
     KW += pos_words;
     if (KW > MAXW) return igx_fail(ctx, IGX_ENOTSUP, "sort: composed key too wide");
@@ -252,6 +258,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     ca.pos_words = pos_words;
     ca.pos_not = pos_not ? 1 : 0;
     ca.pos = pos;
+    ca.pos_stride = pos_stride ? pos_stride : 8;
     ca.valid = valid;
     ca.n = nrows;
     const uint64_t stride = igx_align(nrows, 64);

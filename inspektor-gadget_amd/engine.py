@@ -168,15 +168,44 @@ class Table:
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
 
     def finalize(self):
-        """Synchronises.  Returns dict of device tensors (views into the table):
-        keys (G, key_stride) u8, aggs list of (G,) u64, first (G,) u64, n_groups."""
-        torch = torch_mod()
+        """Synchronises.  Returns the table view (raw device pointers, slot-indexed) as a
+        dict; `groups_ptr` lists the n_groups occupied slots."""
         v = TableView()
         self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
-        G = v.n_groups
-        return {"n_groups": G, "key_bytes": v.key_bytes, "key_stride": v.key_stride,
-                "keys_ptr": v.keys, "aggs_ptr": [v.aggs[i] for i in range(v.naggs)],
-                "first_ptr": v.first_idx, "d_n_groups": v.d_n_groups}
+        self.fin = {"n_groups": v.n_groups, "n_slots": v.n_slots, "key_bytes": v.key_bytes,
+                    "key_stride": v.key_stride, "keys_ptr": v.keys,
+                    "aggs_ptr": [v.aggs[i] for i in range(v.naggs)], "first_ptr": v.first_idx,
+                    "groups_ptr": v.groups, "d_n_groups": v.d_n_groups}
+        return self.fin
+
+    def sort(self, keys, k=0):
+        """igx_groupby_sort: keys = [(src, index_or_(offset,width,kind), desc)].  Returns the
+        first k (0 = all) group slots in SortStats order (device u32)."""
+        torch = torch_mod()
+        ts = []
+        for src, what, desc in keys:
+            if src == _abi.TSRC_KEY:
+                off, w, kind = what
+                ts.append(_abi.TSortKey(src, 0, off, w, kind, int(desc)))
+            else:
+                ts.append(_abi.TSortKey(src, int(what or 0), 0, 0, 0, int(desc)))
+        arr = (_abi.TSortKey * max(1, len(ts)))(*ts)
+        G = self.fin["n_groups"]
+        m = G if k == 0 else min(k, G)
+        out = torch.empty(max(1, m), dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+        if m:
+            self.ctx.check(self.ctx.L.igx_groupby_sort(self.h, arr, len(ts), m, ptr(out)))
+        return out[:m]
+
+    def gather(self, slots):
+        """Packed rows (len(slots), key_bytes + 8*naggs + 8) for the given slots."""
+        torch = torch_mod()
+        row = self.fin["key_bytes"] + 8 * self.naggs + 8
+        k = slots.numel()
+        out = torch.empty((max(1, k), row), dtype=torch.uint8, device=slots.device)
+        if k:
+            self.ctx.check(self.ctx.L.igx_groupby_gather(self.h, ptr(slots), k, ptr(out)))
+        return out[:k]
 
     def destroy(self):
         if self.h:
@@ -191,21 +220,21 @@ class Table:
 
 
 def table_tensors(tab, fin):
-    """Copy the finalized table (device -> device) into torch tensors:
-    keys (G, key_stride) u8, aggs [ (G,) u64 ], first (G,) u64."""
+    """Dense copies of the finalized groups (occupied-slot order) as torch tensors:
+    keys (G, key_bytes) u8, aggs [ (G,) u64 ], first (G,) u64."""
     torch = torch_mod()
     ctx = tab.ctx
     dev = torch.device("cuda", torch.cuda.current_device())
     G = fin["n_groups"]
-    keys = torch.empty((G, fin["key_stride"]), dtype=torch.uint8, device=dev)
-    aggs = [torch.empty(G, dtype=torch.uint64, device=dev) for _ in fin["aggs_ptr"]]
-    first = torch.empty(G, dtype=torch.uint64, device=dev)
+    slots = torch.empty(max(1, G), dtype=torch.int32, device=dev)[:G]
     if G:
-        ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(keys), C.c_void_p(fin["keys_ptr"]),
-                                       G * fin["key_stride"]))
-        for t, p in zip(aggs, fin["aggs_ptr"]):
-            ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(t), C.c_void_p(p), G * 8))
-        ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(first), C.c_void_p(fin["first_ptr"]), G * 8))
+        ctx.check(ctx.L.igx_memcpy_d2d(ctx.h, ptr(slots), C.c_void_p(fin["groups_ptr"]), G * 4))
+    rows = tab.gather(slots)
+    kb = fin["key_bytes"]
+    keys = rows[:, :kb].contiguous()
+    aggs = [rows[:, kb + 8 * i: kb + 8 * i + 8].contiguous().view(torch.uint64).flatten()
+            for i in range(tab.naggs)]
+    first = rows[:, kb + 8 * tab.naggs:].contiguous().view(torch.uint64).flatten()
     return keys, aggs, first
 
 

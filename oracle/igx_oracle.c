@@ -393,6 +393,7 @@ typedef struct {
     const void *cond;    /* condition column */
     u64 cond_val;        /* row counts iff cond == cond_val */
     u32 out_width;       /* wrap width in bytes (1,2,4,8) */
+    u32 val_signed;      /* SUM over a signed column: values sign-extend (Go int64 math) */
 } or_agg;
 
 static inline u64 ld_u(const void *p, u32 w, u64 row) {
@@ -468,6 +469,10 @@ u64 or_groupby(const u8 *keys, u32 kb, u64 n, const u8 *valid, const or_agg *agg
             const or_agg *A = &aggs[a];
             if (A->cond_width && ld_u(A->cond, A->cond_width, i) != A->cond_val) continue;
             u64 add = A->kind == OR_AGG_COUNT ? 1 : ld_u(A->val, A->val_width, i);
+            if (A->kind != OR_AGG_COUNT && A->val_signed && A->val_width < 8) {
+                const u32 sh = 64 - 8 * A->val_width;
+                add = (u64)(((int64_t)(add << sh)) >> sh);
+            }
             u64 *dst = &out_aggs[(u64)a * maxG + g];
             u64 v = *dst + add;
             if (A->out_width < 8) v &= (1ull << (8 * A->out_width)) - 1;

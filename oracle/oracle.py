@@ -418,7 +418,7 @@ def closed_form_perm(key_values, descs, n):
 class _CAgg(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("val_width", C.c_uint32), ("val", C.c_void_p),
                 ("cond_width", C.c_uint32), ("cond", C.c_void_p), ("cond_val", C.c_uint64),
-                ("out_width", C.c_uint32)]
+                ("out_width", C.c_uint32), ("val_signed", C.c_uint32)]
 
 
 def groupby(keys_packed: np.ndarray, aggs, valid=None, base_idx=0, max_groups=None):
@@ -443,7 +443,8 @@ def groupby(keys_packed: np.ndarray, aggs, valid=None, base_idx=0, max_groups=No
                          0 if val is None else val.ctypes.data,
                          0 if cond is None else cond.dtype.itemsize,
                          0 if cond is None else cond.ctypes.data,
-                         int(a.get("cond_val", 0)), int(a.get("out_width", 8))))
+                         int(a.get("cond_val", 0)), int(a.get("out_width", 8)),
+                         int(val is not None and val.dtype.kind == "i")))
     arr = (_CAgg * max(1, len(cag)))(*cag)
     out_keys = np.empty((maxG, kb), dtype=np.uint8)
     out_aggs = np.zeros((max(1, len(aggs)), maxG), dtype=np.uint64)

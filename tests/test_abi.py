@@ -16,7 +16,8 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "igx.h")).read()
-    return sorted(set(re.findall(r"\b(igx_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"^(?:int|const char \*|void \*)\s*(igx_[a-z0-9_]+)\s*\(", src,
+                                 re.MULTILINE)))
 
 
 def test_exports_every_declared_symbol(igx):

@@ -1,0 +1,64 @@
+"""Diagnostics: time k_groupby variants in one process (interleaved rounds) to find where
+the time goes.  Not part of the product path or the tests.
+
+    python tools/ablate_groupby.py --events 100000000 --keys 1000000 --zipf 1.1
+Variants (IGX_GB_DEBUG bits, read per launch): 0 full, 1 load+hash only, 2 stop after the
+LDS lookup (misses dropped), 4 no HBM atomics on misses, 8 full + hit/miss counters.
+"""
+import argparse
+import ctypes as C
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--events", type=int, default=100_000_000)
+    p.add_argument("--keys", type=int, default=1_000_000)
+    p.add_argument("--zipf", type=float, default=1.1)
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--variants", default="0,1,2,4,8")
+    a = p.parse_args()
+    variants = [int(x) for x in a.variants.split(",")]
+    import torch
+    igx = importlib.import_module("inspektor-gadget_amd")
+    from oracle import oracle as O
+    E, H, A = igx.engine, igx.columns, igx._abi
+    N, G = a.events, a.keys
+    cdf = H.to_device(O.zipf_cdf(G, a.zipf))
+    ev = E.gen_tcp(0xC2, 0, G, cdf, 0, N)
+    names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
+    cols = [ev[k] for k in names]
+    tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2],
+                  [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)], G + G // 4)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {}
+    for r in range(a.rounds):
+        for v in variants:
+            os.environ["IGX_GB_DEBUG"] = str(v)
+            tab.reset()
+            e0.record()
+            tab.update(cols, list(range(8)), N, 0)
+            e1.record()
+            torch.cuda.synchronize()
+            res.setdefault(v, []).append(e0.elapsed_time(e1))
+            if v == 8:
+                cnt = (C.c_uint64 * 4)()
+                tab.ctx.check(tab.ctx.L.igx_groupby_debug_counts(tab.h, cnt))
+                res.setdefault("hits_misses", []).append([cnt[0], cnt[1]])
+    os.environ.pop("IGX_GB_DEBUG", None)
+    out = {str(k): (float(np.median(v)) if k != "hits_misses" else v[-1]) for k, v in res.items()}
+    out.update({"events": N, "keys": G, "zipf": a.zipf})
+    print(json.dumps(out))
+    tab.destroy()
+
+
+if __name__ == "__main__":
+    main()
