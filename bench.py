@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+METRIC = "events aggregated/sec (filter+group-by+top-K) at 1/2/4/8 MI355X; % HBM peak"   # BASELINE.json
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")   # tools/pmc_traffic.py
 EV_BYTES = 71                  # saddr16 daddr16 mntns8 pid4 comm16 lport2 dport2 family2 size4 dir1
 GROUP_BYTES = 90               # key 66 + sent 8 + recv 8 + first_idx 8
 
@@ -40,8 +42,8 @@ def parse():
     p.add_argument("--keys", type=int, default=1_000_000, help="key universe per GPU")
     p.add_argument("--zipf", type=float, default=1.1)
     p.add_argument("--topk", type=int, default=20)
-    p.add_argument("--cpu-sample", type=int, default=4_000_000,
-                   help="events in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--cpu-sample", type=int, default=48_000_000,
+                   help="events in the CPU-baseline sample (0 = skip); ~10 s single-thread")
     p.add_argument("--check", action="store_true", help="verify the top-K against the oracle")
     return p.parse_args()
 
@@ -129,6 +131,8 @@ def main():
     alg_bytes = N * EV_BYTES + Gn * GROUP_BYTES
     achieved = alg_bytes / (gb_avg_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = load_traffic(N, G, a.zipf)
+
     check = None
     if a.check and rank == 0 and world == 1:
         check = verify(O, cdf_h, G, N, K, cand, H)
@@ -138,7 +142,7 @@ def main():
         if a.cpu_sample and world == 1:
             cpu = cpu_baseline(O, cdf_h, G, a.cpu_sample, K)
         line = {
-            "metric": "events aggregated/sec (filter+group-by+top-K)",
+            "metric": METRIC,
             "value": value,
             "unit": "events/s",
             "n_gpus": world,
@@ -160,9 +164,12 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_groupby<18>", "kernel_ms": gb_avg_ms,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "k_groupby<ip_key_t>", "kernel_ms": gb_avg_ms,
                 "alg_bytes_per_launch": alg_bytes,
+                "alg_bytes_def": f"{EV_BYTES} B/event x events + {GROUP_BYTES} B/group x groups",
+                "traffic_source": traffic_src,
+                "hbm_pct_of_peak_whole_step": 100.0 * alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
         }
@@ -172,6 +179,20 @@ def main():
     tab.destroy()
     if world > 1:
         dist.destroy_process_group()
+
+
+def load_traffic(N, G, zipf):
+    """HBM bytes per group-by launch measured by rocprofv3 PMC passes for this exact config
+    (tools/pmc_traffic.py output, committed under profiles/); None when absent."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    c = t.get("config", {})
+    if (c.get("events"), c.get("keys"), c.get("zipf")) != (N, G, zipf):
+        return None, None
+    return t["traffic_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT) + " (bytes per launch)"
 
 
 def merge_candidates(E, H, allc, K):

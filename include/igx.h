@@ -177,20 +177,23 @@ typedef struct {
     uint64_t cond_val;
 } igx_agg;
 
-/* The table is an open-addressing array of n_slots records of key_stride bytes; a group's
- * id is its slot.  Record of slot s (at keys + s*key_stride): the packed key, then the
- * slot's first_idx and aggregates at the pointers below + s*key_stride.  groups[0..n_groups)
+/* The table is an open-addressing array of n_slots slots; a group's id is its slot.
+ * Slot s has a key record at keys + s*key_stride (the packed key) and a value record at
+ * first_idx + s*val_stride bytes (u64 first-occurrence index, then the u64 aggregates;
+ * aggs[a] points at slot 0's aggregate a).  Aggregates are kept as u64 sums; they wrap to
+ * their out_width when read (the low out_width bytes, little-endian).  groups[0..n_groups)
  * lists the occupied slots in ascending slot order (the canonical pre-sort order is
  * first_idx, not this). */
 typedef struct {
     uint64_t n_groups;        /* host copy, valid after igx_groupby_finalize */
     uint64_t n_slots;
     uint32_t key_bytes;       /* packed key bytes per group (each key column padded to 4) */
-    uint32_t key_stride;      /* record size: bytes between consecutive slots */
+    uint32_t key_stride;      /* key record size: bytes between consecutive slots' keys */
+    uint32_t val_stride;      /* value record size: bytes between consecutive slots' values */
     uint32_t naggs;
-    const uint8_t *keys;      /* device: slot 0's packed key; n_slots x key_stride */
-    const uint64_t *aggs[16]; /* device: slot 0's aggregate a; stride key_stride */
-    const uint64_t *first_idx;/* device: slot 0's first-occurrence index; stride key_stride */
+    const uint8_t *keys;      /* device: slot 0's packed key */
+    const uint64_t *aggs[16]; /* device: slot 0's aggregate a; stride val_stride */
+    const uint64_t *first_idx;/* device: slot 0's first-occurrence index; stride val_stride */
     const uint32_t *groups;   /* device: occupied slots, n_groups entries */
     const uint64_t *d_n_groups;/* device: group count */
 } igx_table_view;

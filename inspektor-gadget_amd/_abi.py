@@ -51,7 +51,8 @@ class Agg(C.Structure):
 
 class TableView(C.Structure):
     _fields_ = [("n_groups", C.c_uint64), ("n_slots", C.c_uint64), ("key_bytes", C.c_uint32),
-                ("key_stride", C.c_uint32), ("naggs", C.c_uint32), ("keys", C.c_void_p),
+                ("key_stride", C.c_uint32), ("val_stride", C.c_uint32), ("naggs", C.c_uint32),
+                ("keys", C.c_void_p),
                 ("aggs", C.c_void_p * 16), ("first_idx", C.c_void_p), ("groups", C.c_void_p),
                 ("d_n_groups", C.c_void_p)]
 

@@ -7,19 +7,23 @@
 // wrap at their declared width, and each group remembers the global index of its first
 // event -- the canonical pre-sort order that replaces BPF map order.
 //
-// HBM table: S = 2^k records (S >= 2 x capacity), open addressing with linear probing.
-// One record per slot, laid out so a probe touches ONE cache line (R = 64/128 B):
+// HBM table: S = 2^k slots (S >= 2 x capacity), open addressing with linear probing.
+// Each slot has a key record (KR = 32..256 B, one cache line for every built-in layout):
 //     [0, KOFF)            key words (KW x u32, packed; each key column padded to 4 B)
 //     KOFF                 u64 tag   (hash | 1; 0 = empty)
-//     KOFF + 8             u32 ready (key published)
-//     KOFF + 16            u64 first (first-occurrence event index)
-//     KOFF + 24 + 8a       u64 aggregate a
+//     KOFF + 8             u64 ready (0 = key not yet published, else first_ins + 1:
+//                          the claiming event's index, an upper bound of the group's first)
+// and a value record (VR = 8 x 2^m B):  u64 first (first-occurrence event index), then
+// u64 aggregate a at 8 + 8a.  The two are kept apart because 64-bit atomics execute at
+// the memory side and drop their line from L2 (MI355X_MICROARCH.md, store flavours and
+// global atomics): key records are written once per interval and stay L2-resident for
+// the probes, value records only ever receive fire-and-forget atomics.
 // The slot index IS the group id; igx_groupby_finalize lists the occupied slots.
 // A new key claims a record with a 64-bit CAS on the tag, writes its key with write-through
 // (sc1) stores and publishes `ready` with an sc1 store after `s_waitcnt vmcnt(0)`; readers
-// load the record's first KOFF+24 bytes with 16-byte sc1 buffer loads (one round trip)
-// and compare the key in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off
-// table row 1).  No counter is touched per new key.
+// load the key record with 16-byte sc1 buffer loads (one round trip) and compare the key
+// in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off table row 1).  No
+// counter is touched per new key.
 //
 // Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 2-way on the key
 // hash, entries hold the full key, its slot and the workgroup's partial aggregates;
@@ -44,10 +48,13 @@ constexpr uint32_t ST_BUSY = 0xFFFFFFFEu;
 constexpr uint32_t QCAP = 128;   // per-wave miss queue (row ids) in LDS
 
 __host__ __device__ constexpr uint32_t koff_of(int kw) { return (uint32_t)((4 * kw + 7) & ~7); }
-__host__ __device__ constexpr uint32_t rec_bytes(int kw, uint32_t naggs) {
-    const uint32_t b = koff_of(kw) + 24 + 8 * naggs;
-    return b <= 64 ? 64u : ((b + 127) & ~127u);
+__host__ __device__ constexpr uint32_t pow2_at_least(uint32_t b) {
+    uint32_t r = 8;
+    while (r < b) r <<= 1;
+    return r;
 }
+__host__ __device__ constexpr uint32_t krec_bytes(int kw) { return pow2_at_least(koff_of(kw) + 16); }
+__host__ __device__ constexpr uint32_t vrec_bytes(uint32_t naggs) { return pow2_at_least(8 + 8 * naggs); }
 
 // Every input byte is fetched with an unconditional load (no load sits behind a runtime
 // branch), so all of a row's loads issue back to back and retire under one wait.
@@ -75,9 +82,11 @@ struct GbArgs {
     const uint8_t *valid;
     uint64_t n, base_idx;
     // table
-    uint8_t *rec;
-    uint32_t rec_len;       // R
-    uint32_t rec_total;     // S x R (< 2^32)
+    uint8_t *krec;          // key records
+    uint64_t *vrec;         // value records
+    uint32_t krec_len;      // KR
+    uint32_t krec_total;    // S x KR (< 2^32)
+    uint32_t vrec_words;    // VR / 8
     uint32_t *err;
     uint64_t mask;
     uint32_t max_probe;
@@ -216,33 +225,39 @@ __device__ __forceinline__ bool pred_scalar(uint64_t v, uint64_t ref, uint32_t w
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const GbArgs &a) {
-    return __builtin_amdgcn_make_buffer_rsrc(a.rec, (short)0, (int)a.rec_total, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(a.krec, (short)0, (int)a.krec_total, 0x00020000);
 }
 
-// lookup-or-insert in the HBM table; returns the slot (SLOT_OVF: table full).  *first_seen
-// receives the record's first-occurrence index as read (possibly stale-high: it only
-// ever decreases, so it is safe to use to skip an atomicMin).
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+// the first 16*NQ bytes of a key record (key, tag, ready) as sc1 loads (L2-served)
+template <int NQ>
+__device__ __forceinline__ void load_rec(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t (&d)[NQ * 4]) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const u4v q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 16 /* sc1 */);
+        d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w;
+    }
+}
+
+// lookup-or-insert in the HBM table; returns the slot (SLOT_OVF: table full) and the
+// slot's first_ins (claiming event index).  An event with a larger index never needs the
+// atomicMin on the value record's first: the group's first is min(first_ins, that field).
 template <int KW>
 __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
-                                                   uint64_t &first_seen) {
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                                                   uint64_t gidx, uint64_t &first_ins) {
     constexpr uint32_t KOFF = koff_of(KW);
-    constexpr int NQ = (int)((KOFF + 24 + 15) / 16);   // covers key, tag, ready, first
+    constexpr int NQ = (int)((KOFF + 16 + 15) / 16);   // covers key, tag, ready
     const uint64_t tag = h | 1ull;
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     uint64_t s = (h >> 17) & a.mask;
-    first_seen = ~0ull;
     for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
-        const uint32_t off = (uint32_t)(s * a.rec_len);
+        const uint32_t off = (uint32_t)(s * a.krec_len);
         uint32_t d[NQ * 4];
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-            const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 16 /* sc1 */);
-            d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w;
-        }
-        uint8_t *r = a.rec + off;
+        load_rec<NQ>(rs, off, d);
+        uint8_t *r = a.krec + off;
         uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
-        uint32_t ready = d[KOFF / 4 + 2];
+        uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
         if (t == 0) {
             const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF), 0ull,
                                            (unsigned long long)tag);
@@ -255,7 +270,8 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                         st_agent(reinterpret_cast<uint32_t *>(r + 4 * w), k[w]);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(reinterpret_cast<uint32_t *>(r + KOFF + 8), 1u);
+                st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), gidx + 1);
+                first_ins = gidx;
                 return (uint32_t)s;
             }
             t = old;
@@ -264,24 +280,29 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
         if (t == tag) {
             if (!ready) {
                 uint32_t spins = 0;
-                while (ld_agent(reinterpret_cast<const uint32_t *>(r + KOFF + 8)) == 0) {
+                while (ld_agent(reinterpret_cast<const uint64_t *>(r + KOFF + 8)) == 0) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1u << 22)) {
                         atomicOr(a.err, 2u);
                         return SLOT_OVF;
                     }
                 }
-#pragma unroll
-                for (int i = 0; i < NQ; ++i) {
-                    const u4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 16);
-                    d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w;
-                }
+                load_rec<NQ>(rs, off, d);
             }
             bool eq = true;
 #pragma unroll
             for (int w = 0; w < KW; ++w) eq = eq && (d[w] == k[w]);
+            if (!eq) {
+                // The quads of one snapshot are separate loads: `ready` may have been sampled
+                // after the key quads, so a tag hit with a key mismatch is re-read once, now
+                // ordered after the ready observation (genuine 64-bit tag collisions are rare).
+                load_rec<NQ>(rs, off, d);
+                eq = true;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) eq = eq && (d[w] == k[w]);
+            }
             if (eq) {
-                first_seen = (uint64_t)d[KOFF / 4 + 4] | ((uint64_t)d[KOFF / 4 + 5] << 32);
+                first_ins = ((uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32)) - 1;
                 return (uint32_t)s;
             }
         }
@@ -355,29 +376,32 @@ __device__ __forceinline__ bool load_row(const GbArgs &a, uint64_t row, uint32_t
     return ok;
 }
 
+// LDS probing: linear over LDS_PROBE entries from the hash's home entry.  Entries are never
+// evicted, so an EMPTY entry ends the search (a key being adopted right now may be missed:
+// its event then takes the HBM path, which is only slower).
+constexpr int LDS_PROBE = 8;
+
 template <int KW>
 __device__ __forceinline__ int lds_lookup(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t &gs) {
-    const uint32_t e0 = (uint32_t)(h >> 40) & (c.E - 1);
-    int slot = -1;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const uint32_t e = e0 ^ (uint32_t)j;
+    const uint32_t e0 = (uint32_t)(h >> 40);
+    for (int j = 0; j < LDS_PROBE; ++j) {
+        const uint32_t e = (e0 + (uint32_t)j) & (c.E - 1);
         const uint32_t s = __hip_atomic_load(&c.st[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (slot < 0 && s < ST_BUSY && c.tag[e] == h && lds_key_eq<KW>(c, e, k)) {
-            slot = (int)e;
+        if (s == ST_EMPTY) break;
+        if (s < ST_BUSY && c.tag[e] == h && lds_key_eq<KW>(c, e, k)) {
             gs = s;
+            return (int)e;
         }
     }
-    return slot;
+    return -1;
 }
 
 // adopt an empty LDS entry for a key just resolved in HBM (first come, never evicted)
 template <int KW>
 __device__ __forceinline__ int lds_adopt(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t gs) {
-    const uint32_t e0 = (uint32_t)(h >> 40) & (c.E - 1);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const uint32_t e = e0 ^ (uint32_t)j;
+    const uint32_t e0 = (uint32_t)(h >> 40);
+    for (int j = 0; j < LDS_PROBE; ++j) {
+        const uint32_t e = (e0 + (uint32_t)j) & (c.E - 1);
         if (c.st[e] == ST_EMPTY) {
             if (atomicCAS(&c.st[e], ST_EMPTY, ST_BUSY) == ST_EMPTY) {
                 c.tag[e] = h;
@@ -393,16 +417,16 @@ __device__ __forceinline__ int lds_adopt(const LdsCache<KW> &c, const uint32_t (
     return -1;
 }
 
-__device__ __forceinline__ uint64_t *rec_first(const GbArgs &a, uint32_t gs, uint32_t koff) {
-    return reinterpret_cast<uint64_t *>(a.rec + (uint64_t)gs * a.rec_len + koff + 16);
+__device__ __forceinline__ unsigned long long *rec_first(const GbArgs &a, uint32_t gs) {
+    return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words);
 }
-__device__ __forceinline__ uint64_t *rec_agg(const GbArgs &a, uint32_t gs, uint32_t koff, int x) {
-    return reinterpret_cast<uint64_t *>(a.rec + (uint64_t)gs * a.rec_len + koff + 24 + 8 * x);
+__device__ __forceinline__ unsigned long long *rec_agg(const GbArgs &a, uint32_t gs, int x) {
+    return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words + 1 + x);
 }
 
 template <int KW>
 __device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &c, int slot, uint32_t gs,
-                                           const uint64_t (&v)[AMAX], uint64_t gidx, uint64_t first_seen) {
+                                           const uint64_t (&v)[AMAX], uint64_t gidx, uint64_t first_ins) {
     if (slot >= 0) {
 #pragma unroll
         for (int x = 0; x < AMAX; ++x)
@@ -410,13 +434,10 @@ __device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &
                 atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
         atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
     } else if (!(a.dbg & 4u)) {
-        constexpr uint32_t KOFF = koff_of(KW);
 #pragma unroll
         for (int x = 0; x < AMAX; ++x)
-            if (x < (int)a.naggs && v[x])
-                atomicAdd(reinterpret_cast<unsigned long long *>(rec_agg(a, gs, KOFF, x)), (unsigned long long)v[x]);
-        if (first_seen > gidx)
-            atomicMin(reinterpret_cast<unsigned long long *>(rec_first(a, gs, KOFF)), (unsigned long long)gidx);
+            if (x < (int)a.naggs && v[x]) atomicAdd(rec_agg(a, gs, x), (unsigned long long)v[x]);
+        if (gidx < first_ins) atomicMin(rec_first(a, gs), (unsigned long long)gidx);
     }
 }
 
@@ -433,13 +454,14 @@ __device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::
         (void)load_row<L>(a, row, k, v);      // predicates already passed
         const uint64_t h = hash_key<KW>(k);
         uint32_t gs = SLOT_OVF;
-        uint64_t first_seen = ~0ull;
+        uint64_t first_ins = 0;
+        const uint64_t gidx = a.base_idx + row;
         int slot = lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
         if (slot < 0) {
-            gs = find_or_insert<KW>(a, k, h, first_seen);
+            gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
             if (gs != SLOT_OVF) slot = lds_adopt<KW>(c, k, h, gs);
         }
-        if (gs != SLOT_OVF) accumulate<KW>(a, c, slot, gs, v, a.base_idx + row, first_seen);
+        if (gs != SLOT_OVF) accumulate<KW>(a, c, slot, gs, v, gidx, first_ins);
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -502,30 +524,29 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     }
 
     __syncthreads();
-    constexpr uint32_t KOFF = koff_of(KW);
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         const uint32_t gs = c.st[e];
         if (gs >= ST_BUSY) continue;
         for (uint32_t x = 0; x < a.naggs; ++x) {
             const uint64_t s = c.agg[x * E + e];
-            if (s) atomicAdd(reinterpret_cast<unsigned long long *>(rec_agg(a, gs, KOFF, (int)x)), (unsigned long long)s);
+            if (s) atomicAdd(rec_agg(a, gs, (int)x), (unsigned long long)s);
         }
         const uint64_t f = c.first[e];
-        if (ld_agent(rec_first(a, gs, KOFF)) > f)
-            atomicMin(reinterpret_cast<unsigned long long *>(rec_first(a, gs, KOFF)), (unsigned long long)f);
+        const uint64_t fi = ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
+                                                                        koff_of(KW) + 8)) - 1;
+        if (f < fi) atomicMin(rec_first(a, gs), (unsigned long long)f);
     }
 }
 
 // per-interval reset: tag/ready = 0, first = ~0, aggregates = 0 (keys are left as is)
-__global__ void k_table_reset(uint8_t *rec, uint32_t rec_len, uint32_t koff, uint32_t naggs, uint64_t ns,
-                              uint32_t *err) {
+__global__ void k_table_reset(uint8_t *krec, uint32_t krec_len, uint32_t koff, uint64_t *vrec, uint32_t vw,
+                              uint64_t ns, uint32_t *err) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-        uint64_t *h = reinterpret_cast<uint64_t *>(rec + i * rec_len + koff);
-        h[0] = 0;
-        h[1] = 0;
-        h[2] = ~0ull;
-        for (uint32_t x = 0; x < naggs; ++x) h[3 + x] = 0;
+        *reinterpret_cast<uint4 *>(krec + i * krec_len + koff) = make_uint4(0, 0, 0, 0);
+        uint64_t *v = vrec + i * vw;
+        v[0] = ~0ull;
+        for (uint32_t x = 1; x < vw; ++x) v[x] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;
 }
@@ -605,28 +626,41 @@ __global__ __launch_bounds__(256) void k_slots_write(const uint8_t *__restrict__
     }
 }
 
+// first = min(value record's first, key record's first_ins) for every listed group
+__global__ void k_fold_first(const uint8_t *__restrict__ krec, uint32_t krec_len, uint32_t koff,
+                             uint64_t *__restrict__ vrec, uint32_t vw, const uint32_t *__restrict__ groups,
+                             uint64_t ng) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = groups[i];
+        const uint64_t fi = *reinterpret_cast<const uint64_t *>(krec + (uint64_t)g * krec_len + koff + 8) - 1;
+        uint64_t *f = vrec + (uint64_t)g * vw;
+        if (fi < *f) *f = fi;
+    }
+}
+
 // materialise selected groups as packed rows key | aggs | first (the Stats rows of
 // nextStats, tracer.go:186-219); aggregates wrap to their out_width (the BPF value width)
 struct AggMasks {
     uint32_t m[2 * AMAX];   // (lo, hi) word masks per aggregate
 };
 
-__global__ void k_gather_rows(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff, uint32_t key_words,
-                              uint32_t naggs, AggMasks am, const uint32_t *__restrict__ idx, uint64_t ns, uint64_t k,
-                              uint8_t *__restrict__ out) {
+__global__ void k_gather_rows(const uint8_t *__restrict__ krec, uint32_t krec_len, const uint64_t *__restrict__ vrec,
+                              uint32_t vw, uint32_t key_words, uint32_t naggs, AggMasks am,
+                              const uint32_t *__restrict__ idx, uint64_t ns, uint64_t k, uint8_t *__restrict__ out) {
     const uint64_t r = blockIdx.x;
     if (r >= k) return;
     const uint32_t row_words = key_words + 2 * naggs + 2;
     uint32_t *o = reinterpret_cast<uint32_t *>(out) + r * row_words;
     const uint32_t g = idx[r];
     const bool ok = g < ns;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(rec + (uint64_t)g * rec_len);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(krec + (uint64_t)g * krec_len);
+    const uint32_t *val = reinterpret_cast<const uint32_t *>(vrec + (uint64_t)g * vw);
     for (uint32_t w = threadIdx.x; w < row_words; w += blockDim.x) {
         uint32_t v = 0;
         if (ok) {
             if (w < key_words) v = src[w];
-            else if (w < key_words + 2 * naggs) v = src[(koff + 24) / 4 + (w - key_words)] & am.m[w - key_words];
-            else v = src[(koff + 16) / 4 + (w - key_words - 2 * naggs)];
+            else if (w < key_words + 2 * naggs) v = val[2 + (w - key_words)] & am.m[w - key_words];
+            else v = val[w - key_words - 2 * naggs];
         }
         o[w] = v;
     }
@@ -643,13 +677,14 @@ struct igx_table {
     uint32_t key_widths[32] = {};
     uint32_t key_words = 0;      // packed words (each column padded to 4 B)
     uint32_t kw_rec = 0;         // key words as the kernel lays them out (static KW or generic width)
-    uint32_t koff = 0, rec_len = 0;
+    uint32_t koff = 0, krec_len = 0, vrec_len = 0;
     bool generic = false;        // no compile-time layout (or IGX_GB_GENERIC at create)
     igx_agg aggs[AMAX] = {};
     uint32_t naggs = 0;
     uint64_t cap = 0;            // distinct keys promised by the caller
     uint64_t nslots = 0;
-    uint8_t *rec = nullptr;
+    uint8_t *krec = nullptr;
+    uint64_t *vrec = nullptr;
     uint32_t *err = nullptr;
     uint32_t *groups = nullptr;  // occupied slots after finalize
     uint32_t *tile_cnt = nullptr;
@@ -723,22 +758,24 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
             }
     }
     t->koff = koff_of((int)t->kw_rec);
-    t->rec_len = rec_bytes((int)t->kw_rec, naggs);
+    t->krec_len = krec_bytes((int)t->kw_rec);
+    t->vrec_len = vrec_bytes(naggs);
     t->naggs = naggs;
     for (uint32_t i = 0; i < naggs; ++i) t->aggs[i] = aggs[i];
     t->cap = capacity;
     uint64_t ns = 1024;
     while (ns < 2 * capacity) ns <<= 1;
     t->nslots = ns;
-    if (ns * t->rec_len >= (1ull << 32)) {
-        const uint32_t r = t->rec_len;
+    if (ns * t->krec_len >= (1ull << 32)) {
+        const uint32_t r = t->krec_len;
         delete t;
         return igx_fail(ctx, IGX_ENOTSUP, "groupby_create: table of %llu x %u B exceeds 4 GiB",
                         (unsigned long long)ns, r);
     }
     const uint64_t tiles = (ns + CT - 1) / CT;
-    hipError_t e = hipMalloc(&t->rec, ns * t->rec_len);
-    if (e == hipSuccess) e = hipMemsetAsync(t->rec, 0, ns * t->rec_len, ctx->stream);
+    hipError_t e = hipMalloc(&t->krec, ns * t->krec_len);
+    if (e == hipSuccess) e = hipMemsetAsync(t->krec, 0, ns * t->krec_len, ctx->stream);
+    if (e == hipSuccess) e = hipMalloc(&t->vrec, ns * t->vrec_len);
     if (e == hipSuccess) e = hipMalloc(&t->err, 64);
     if (e == hipSuccess) e = hipMalloc(&t->groups, ns * 4);
     if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
@@ -756,8 +793,8 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
 extern "C" int igx_groupby_reset(igx_table *t) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    hipLaunchKernelGGL(k_table_reset, dim3(2048), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff, t->naggs,
-                       t->nslots, t->err);
+    hipLaunchKernelGGL(k_table_reset, dim3(2048), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff, t->vrec,
+                       t->vrec_len / 8, t->nslots, t->err);
     IGX_HIP(ctx, hipGetLastError());
     t->host_groups = 0;
     return IGX_OK;
@@ -766,7 +803,8 @@ extern "C" int igx_groupby_reset(igx_table *t) {
 extern "C" int igx_groupby_destroy(igx_table *t) {
     if (!t) return IGX_OK;
     (void)hipStreamSynchronize(t->ctx->stream);
-    (void)hipFree(t->rec);
+    (void)hipFree(t->krec);
+    (void)hipFree(t->vrec);
     (void)hipFree(t->err);
     (void)hipFree(t->groups);
     (void)hipFree(t->tile_cnt);
@@ -882,9 +920,11 @@ extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t nc
     a.valid = nullptr;
     a.n = nrows;
     a.base_idx = base_idx;
-    a.rec = t->rec;
-    a.rec_len = t->rec_len;
-    a.rec_total = (uint32_t)(t->nslots * t->rec_len);
+    a.krec = t->krec;
+    a.vrec = t->vrec;
+    a.krec_len = t->krec_len;
+    a.krec_total = (uint32_t)(t->nslots * t->krec_len);
+    a.vrec_words = t->vrec_len / 8;
     a.err = t->err;
     a.mask = t->nslots - 1;
     a.max_probe = (uint32_t)std::min<uint64_t>(t->nslots, 1u << 20);
@@ -923,10 +963,10 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     const uint64_t tiles = (t->nslots + CT - 1) / CT;
-    hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff,
+    hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
                        t->nslots, t->tile_cnt);
     hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups);
-    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->rec, t->rec_len, t->koff,
+    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
                        t->nslots, t->tile_cnt, t->groups);
     IGX_HIP(ctx, hipGetLastError());
     uint64_t *h;
@@ -938,16 +978,22 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     const uint64_t ng = h[0];
     const uint32_t err = reinterpret_cast<uint32_t *>(h)[2];
     t->host_groups = ng;
+    if (ng && !err) {
+        const uint32_t fb = (uint32_t)std::min<uint64_t>(4096, (ng + 255) / 256);
+        hipLaunchKernelGGL(k_fold_first, dim3(fb), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff, t->vrec,
+                           t->vrec_len / 8, t->groups, ng);
+        IGX_HIP(ctx, hipGetLastError());
+    }
     if (view) {
         view->n_groups = ng;
         view->n_slots = t->nslots;
         view->key_bytes = t->key_words * 4;
-        view->key_stride = t->rec_len;
+        view->key_stride = t->krec_len;
+        view->val_stride = t->vrec_len;
         view->naggs = t->naggs;
-        view->keys = t->rec;
-        for (uint32_t x = 0; x < 16; ++x)
-            view->aggs[x] = x < t->naggs ? reinterpret_cast<const uint64_t *>(t->rec + t->koff + 24 + 8 * x) : nullptr;
-        view->first_idx = reinterpret_cast<const uint64_t *>(t->rec + t->koff + 16);
+        view->keys = t->krec;
+        for (uint32_t x = 0; x < 16; ++x) view->aggs[x] = x < t->naggs ? t->vrec + 1 + x : nullptr;
+        view->first_idx = t->vrec;
         view->groups = t->groups;
         view->d_n_groups = t->n_groups;
     }
@@ -970,8 +1016,8 @@ extern "C" int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k,
         am.m[2 * x] = (uint32_t)m;
         am.m[2 * x + 1] = (uint32_t)(m >> 32);
     }
-    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)k), dim3(64), 0, ctx->stream, t->rec, t->rec_len, t->koff,
-                       t->key_words, t->naggs, am, idx, t->nslots, k, out_rows);
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)k), dim3(64), 0, ctx->stream, t->krec, t->krec_len, t->vrec,
+                       t->vrec_len / 8, t->key_words, t->naggs, am, idx, t->nslots, k, out_rows);
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }
@@ -989,20 +1035,21 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
         const igx_tsortkey &q = keys[i];
         sk[i] = igx_sortkey{};
         sk[i].desc = q.desc;
-        strides[i] = t->rec_len;
+        strides[i] = t->vrec_len;
         if (q.src == IGX_TSRC_AGG) {
             if (q.index >= t->naggs) return igx_fail(ctx, IGX_EINVAL, "groupby_sort: aggregate %u", q.index);
-            sk[i].ptr = t->rec + t->koff + 24 + 8 * q.index;   // little endian: the low out_width bytes
+            sk[i].ptr = t->vrec + 1 + q.index;   // little endian: the low out_width bytes
             sk[i].width = t->aggs[q.index].out_width ? t->aggs[q.index].out_width : 8;   // are the wrapped value
             sk[i].kind = IGX_KIND_UINT;
         } else if (q.src == IGX_TSRC_FIRST) {
-            sk[i].ptr = t->rec + t->koff + 16;
+            sk[i].ptr = t->vrec;
             sk[i].width = 8;
             sk[i].kind = IGX_KIND_UINT;
         } else if (q.src == IGX_TSRC_KEY) {
             if (q.offset + q.width > t->key_words * 4)
                 return igx_fail(ctx, IGX_EINVAL, "groupby_sort: key bytes out of range");
-            sk[i].ptr = t->rec + q.offset;
+            sk[i].ptr = t->krec + q.offset;
+            strides[i] = t->krec_len;
             sk[i].width = q.width;
             sk[i].kind = q.kind;
         } else {
@@ -1010,7 +1057,7 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
         }
     }
     return sort_common_rows(ctx, sk, strides, nkeys, t->host_groups, t->groups,
-                            reinterpret_cast<const uint64_t *>(t->rec + t->koff + 16), t->rec_len, k, out_slots);
+                            t->vrec, t->vrec_len, k, out_slots);
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.

@@ -151,27 +151,86 @@ __global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ 
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan in place over m u32 values, one block of 1024 threads
-__global__ __launch_bounds__(1024) void k_scan_inplace(uint32_t *__restrict__ v, uint64_t m) {
-    __shared__ uint32_t part[1024];
-    const uint64_t per = (m + 1023) / 1024;
-    const uint64_t b = threadIdx.x * per, e = min(m, b + per);
-    uint32_t s = 0;
-    for (uint64_t i = b; i < e; ++i) s += v[i];
-    part[threadIdx.x] = s;
+// Three-phase exclusive scan over m u32 values (the [digit][tile] histogram): per-chunk
+// sums, one block scanning the chunk sums, per-chunk scans with their carry.
+constexpr uint32_t SCAN_CHUNK = 4096;   // 1024 threads x 4
+
+__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t v, uint32_t *tmp, uint32_t &total) {
+    // tmp: 16 words of LDS; wave-level inclusive scan then wave totals
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) tmp[wave] = x;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        uint32_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
+    uint32_t wpre = 0;
+    total = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+        const uint32_t t = tmp[w];
+        if (w < wave) wpre += t;
+        total += t;
     }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (uint64_t i = b; i < e; ++i) {
-        uint32_t c = v[i];
-        v[i] = run;
-        run += c;
+    __syncthreads();
+    return wpre + x - v;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t *__restrict__ v, uint64_t m,
+                                                      uint32_t *__restrict__ part) {
+    __shared__ uint32_t tmp[16];
+    const uint64_t b = (uint64_t)blockIdx.x * SCAN_CHUNK + 4 * threadIdx.x;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += (b + j < m) ? v[b + j] : 0u;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; ++w) t += tmp[w];
+        part[blockIdx.x] = t;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_parts(uint32_t *__restrict__ part, uint32_t np) {
+    __shared__ uint32_t tmp[16];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < np; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < np ? part[i] : 0u;
+        uint32_t total;
+        const uint32_t e = block_excl_scan_1024(v, tmp, total);
+        if (i < np) part[i] = carry + e;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_apply(uint32_t *__restrict__ v, uint64_t m,
+                                                     const uint32_t *__restrict__ part) {
+    __shared__ uint32_t tmp[16];
+    const uint64_t b = (uint64_t)blockIdx.x * SCAN_CHUNK + 4 * threadIdx.x;
+    uint32_t x[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        x[j] = (b + j < m) ? v[b + j] : 0u;
+        s += x[j];
+    }
+    uint32_t total;
+    uint32_t run = part[blockIdx.x] + block_excl_scan_1024(s, tmp, total);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (b + j < m) v[b + j] = run;
+        run += x[j];
+    }
+}
+
+static void launch_scan(hipStream_t st, uint32_t *v, uint64_t m, uint32_t *part) {
+    const uint32_t np = (uint32_t)((m + SCAN_CHUNK - 1) / SCAN_CHUNK);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(np), dim3(1024), 0, st, v, m, part);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, np);
+    hipLaunchKernelGGL(k_scan_apply, dim3(np), dim3(1024), 0, st, v, m, part);
 }
 
 struct ScatterArgs {
@@ -230,6 +289,115 @@ __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
     }
 }
 
+
+// ---- top-K by radix select (k <= SEL_SMALL_K) -----------------------------------------
+// The composed keys are unique (the position word is part of them), so the k smallest
+// rows form an exact set.  Each pass histograms a 12-bit digit of the candidates
+// (MSB first, starting at the first bit that varies), keeps every row whose digit is below
+// the bin holding the k-th row and carries the rows of that bin to the next pass.  The
+// accepted k rows are then ranked against each other (one workgroup per row).
+constexpr int SEL_BITS = 12;
+constexpr uint32_t SEL_BINS = 1u << SEL_BITS;
+constexpr uint32_t SEL_SMALL_K = 4096;
+
+__device__ __forceinline__ uint32_t sel_digit(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                              uint64_t i, uint32_t bitpos, uint32_t nbits) {
+    const uint32_t w = bitpos >> 5, o = bitpos & 31;
+    const uint64_t hi = W[(uint64_t)w * stride + i];
+    const uint64_t lo = (w + 1 < nw) ? W[(uint64_t)(w + 1) * stride + i] : 0ull;
+    const uint64_t x = (hi << 32) | lo;
+    return (uint32_t)((x << o) >> (64 - nbits));
+}
+
+__global__ __launch_bounds__(TB) void k_sel_hist(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                 const uint32_t *__restrict__ cand, uint64_t n, uint32_t bitpos,
+                                                 uint32_t nbits, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[SEL_BINS];
+    for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB) h[b] = 0;
+    __syncthreads();
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < n; j += (uint64_t)gridDim.x * TB) {
+        const uint64_t i = cand ? cand[j] : j;
+        atomicAdd(&h[sel_digit(W, stride, nw, i, bitpos, nbits)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB)
+        if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// rows with digit < b -> acc (appended), digit == b -> out (next candidates).  One global
+// reservation per workgroup and list (a single returning atomic word saturates quickly).
+__global__ __launch_bounds__(TB) void k_sel_split(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                  const uint32_t *__restrict__ cand, uint64_t n, uint32_t bitpos,
+                                                  uint32_t nbits, uint32_t b, uint32_t *__restrict__ acc,
+                                                  uint32_t *__restrict__ acc_cnt, uint32_t *__restrict__ out,
+                                                  uint32_t *__restrict__ out_cnt) {
+    __shared__ uint32_t lcnt[2], gbase[2];
+    if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t row[IPT], pos[IPT];
+    uint32_t kind[IPT];   // 0 drop, 1 accept, 2 carry
+    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t q = tbase + (uint64_t)j * TB + threadIdx.x;
+        kind[j] = 0;
+        row[j] = 0;
+        if (q < n) {
+            row[j] = cand ? cand[q] : (uint32_t)q;
+            const uint32_t d = sel_digit(W, stride, nw, row[j], bitpos, nbits);
+            kind[j] = d < b ? 1u : (d == b ? 2u : 0u);
+        }
+        const uint64_t m1 = __ballot(kind[j] == 1), m2 = __ballot(kind[j] == 2);
+        uint32_t b1 = 0, b2 = 0;
+        if (lane == 0) {
+            if (m1) b1 = atomicAdd(&lcnt[0], (uint32_t)__popcll(m1));
+            if (m2) b2 = atomicAdd(&lcnt[1], (uint32_t)__popcll(m2));
+        }
+        b1 = __shfl(b1, 0);
+        b2 = __shfl(b2, 0);
+        pos[j] = kind[j] == 1 ? b1 + __popcll(m1 & lanemask_lt()) : b2 + __popcll(m2 & lanemask_lt());
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        gbase[0] = lcnt[0] ? atomicAdd(acc_cnt, lcnt[0]) : 0;
+        gbase[1] = lcnt[1] ? atomicAdd(out_cnt, lcnt[1]) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (kind[j] == 1) acc[gbase[0] + pos[j]] = row[j];
+        else if (kind[j] == 2) out[gbase[1] + pos[j]] = row[j];
+    }
+}
+
+// rank of acc[r] among the k accepted rows (full composed-key compare) -> out_perm
+__global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                 const uint32_t *__restrict__ acc, uint32_t k,
+                                                 const uint32_t *__restrict__ payload, uint32_t *__restrict__ out) {
+    __shared__ uint32_t red[TB / 64];
+    const uint32_t r = blockIdx.x;
+    const uint32_t me = acc[r];
+    uint32_t less = 0;
+    for (uint32_t j = threadIdx.x; j < k; j += TB) {
+        const uint32_t o = acc[j];
+        int c = 0;
+        for (uint32_t w = 0; w < nw && c == 0; ++w) {
+            const uint32_t x = W[(uint64_t)w * stride + o], y = W[(uint64_t)w * stride + me];
+            c = x < y ? -1 : (x > y ? 1 : 0);
+        }
+        less += c < 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) less += __shfl_xor(less, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = less;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < TB / 64; ++w) t += red[w];
+        out[t] = payload[me];
+    }
+}
+
 }  // namespace
 
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
@@ -267,16 +435,20 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const uint32_t nblocks = (uint32_t)((nrows + TILE - 1) / TILE);
     const size_t words_b = igx_align((size_t)KW * stride * 4, 256);
     const size_t pay_b = igx_align(stride * 4, 256);
-    const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256);
+    const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
+                          igx_align(((size_t)256 * nblocks + SCAN_CHUNK - 1) / SCAN_CHUNK * 4, 256);
     const size_t res_b = igx_align((size_t)KW * 8, 256);
+    const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
+    const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     void *s;
-    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b, &s);
+    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b, &s);
     if (rc) return rc;
     char *c = reinterpret_cast<char *>(s);
     uint32_t *W[2] = {reinterpret_cast<uint32_t *>(c), reinterpret_cast<uint32_t *>(c + words_b)};
     uint32_t *P[2] = {reinterpret_cast<uint32_t *>(c + 2 * words_b),
                       reinterpret_cast<uint32_t *>(c + 2 * words_b + pay_b)};
     uint32_t *hist = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b);
+    uint32_t *scan_part = hist + igx_align((size_t)256 * nblocks, 64);
     uint32_t *res = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b);
 
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
@@ -289,6 +461,63 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     if (rc) return rc;
     IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+
+    if (use_sel) {
+        // top-K: radix select on the composed keys, then rank the k survivors
+        uint32_t bitpos = KW * 32;
+        for (uint32_t w = 0; w < KW; ++w) {
+            const uint32_t diff = hres[2 * w] ^ hres[2 * w + 1];
+            if (diff) {
+                bitpos = 32 * w + (uint32_t)__builtin_clz(diff);
+                break;
+            }
+        }
+        // selection scratch: acc | cand A | cand B | counters | hist
+        uint32_t *acc = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b);
+        uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
+        uint32_t *cnt = cnd[1] + stride;            // [0] acc count, [1] next-candidate count
+        uint32_t *dh = cnt + 64;                    // SEL_BINS
+        uint32_t *hh;
+        rc = igx_pinned(ctx, SEL_BINS * 4 + 64, reinterpret_cast<void **>(&hh));
+        if (rc) return rc;
+        IGX_HIP(ctx, hipMemsetAsync(cnt, 0, 8, ctx->stream));
+        const uint32_t *cand = nullptr;
+        uint64_t n = nrows;
+        uint32_t krem = limit, cur_c = 0;
+        while (n > krem) {
+            if (bitpos >= KW * 32) return igx_fail(ctx, IGX_EIO, "topk: composed keys not unique");
+            const uint32_t nbits = std::min<uint32_t>(SEL_BITS, KW * 32 - bitpos);
+            IGX_HIP(ctx, hipMemsetAsync(dh, 0, SEL_BINS * 4, ctx->stream));
+            const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, (n + TB - 1) / TB);
+            hipLaunchKernelGGL(k_sel_hist, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, cand, n, bitpos,
+                               nbits, dh);
+            IGX_HIP(ctx, hipMemcpyAsync(hh, dh, SEL_BINS * 4, hipMemcpyDeviceToHost, ctx->stream));
+            IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            uint32_t b = 0;
+            uint64_t below = 0;
+            for (; b < (1u << nbits); ++b) {
+                if (below + hh[b] >= krem) break;
+                below += hh[b];
+            }
+            uint32_t *nxt = cnd[cur_c];
+            IGX_HIP(ctx, hipMemsetAsync(cnt + 1, 0, 4, ctx->stream));
+            const uint32_t sb = (uint32_t)((n + TILE - 1) / TILE);
+            hipLaunchKernelGGL(k_sel_split, dim3(sb), dim3(TB), 0, ctx->stream, W[0], stride, KW, cand, n, bitpos,
+                               nbits, b, acc, cnt, nxt, cnt + 1);
+            krem -= (uint32_t)below;
+            n = hh[b];
+            cand = nxt;
+            cur_c ^= 1;
+            bitpos += nbits;
+        }
+        if (krem)   // every remaining candidate is in (n == krem); limit - krem were accepted
+            IGX_HIP(ctx, hipMemcpyAsync(acc + (limit - krem), cand, (size_t)krem * 4, hipMemcpyDeviceToDevice,
+                                        ctx->stream));
+        hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
+                           out_perm);
+        IGX_HIP(ctx, hipGetLastError());
+        return IGX_OK;
+    }
 
     // digit plan: word w (0 = most significant), byte b (0 = least significant in word)
     std::vector<int> live_word(KW, 0);
@@ -320,8 +549,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             sa.pout = P[cur ^ 1];
             hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(TB), 0, ctx->stream,
                                sa.in[dslot], sa.shift, nrows, nblocks, hist);
-            hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, ctx->stream, hist,
-                               (uint64_t)256 * nblocks);
+            launch_scan(ctx->stream, hist, (uint64_t)256 * nblocks, scan_part);
             hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
             // swap buffers: the next pass reads what this one wrote
             cur ^= 1;

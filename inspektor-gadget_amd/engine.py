@@ -173,7 +173,7 @@ class Table:
         v = TableView()
         self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
         self.fin = {"n_groups": v.n_groups, "n_slots": v.n_slots, "key_bytes": v.key_bytes,
-                    "key_stride": v.key_stride, "keys_ptr": v.keys,
+                    "key_stride": v.key_stride, "val_stride": v.val_stride, "keys_ptr": v.keys,
                     "aggs_ptr": [v.aggs[i] for i in range(v.naggs)], "first_ptr": v.first_idx,
                     "groups_ptr": v.groups, "d_n_groups": v.d_n_groups}
         return self.fin

@@ -47,8 +47,10 @@ def _pred(A, col, cmp, value, dtype, negate=False):
 def _check(E, H, tab, widths, okeys, oaggs, ofirst):
     fin = tab.finalize()
     keys, aggs, first = E.table_tensors(tab, fin)
-    assert fin["n_groups"] == len(okeys)
     gk = _unpad(H.host(keys), widths)
+    distinct = len({bytes(k) for k in gk})
+    assert distinct == len(gk), f"{len(gk) - distinct} duplicate groups"
+    assert fin["n_groups"] == len(okeys)
     ga = [H.host(a) for a in aggs]
     gf = H.host(first)
     ref = {bytes(k): tuple(int(a[i]) for a in oaggs) + (int(ofirst[i]),) for i, k in enumerate(okeys)}

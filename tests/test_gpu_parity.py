@@ -149,6 +149,11 @@ def test_ties_and_parity(oracle, E, H, torch):
         got = H.host(E.sort_perm(keys_d, n))
         ref = oracle.go_sort_entries(keys_o, n)
         assert np.array_equal(got, ref), (trial, kinds)
+        # top-K (radix-select path when n > 2k): the first k of the same order
+        for k in (1, 7, 300):
+            if n > k:
+                top = H.host(E.sort_perm(keys_d, n, k=k))
+                assert np.array_equal(top, ref[:k]), (trial, kinds, k)
 
 
 def test_filter_c1(oracle, E, H, igx, torch):
