@@ -1,0 +1,15 @@
+# Round-1 profile: kernel trace + stats, HBM traffic PMC passes, then the default bench.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out profiles/r01
+B="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- $B > gpurun_out/prof.log 2>&1 || { echo "rocprof trace failed rc=$?"; tail gpurun_out/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o p -- $B > gpurun_out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed rc=$?"; tail gpurun_out/pmc_fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o p -- $B > gpurun_out/pmc_write.log 2>&1 || { echo "pmc write failed rc=$?"; tail gpurun_out/pmc_write.log; exit 1; }
+python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --kernel k_groupby \
+  --config '{"events": 100000000, "keys": 1000000, "zipf": 1.1}' --out gpurun_out/traffic.json || { echo "traffic parse failed"; exit 1; }
+cp gpurun_out/traffic.json profiles/r01/traffic.json
+timeout -k 10 600 python3 bench.py > gpurun_out/bench_full.log 2>&1 || { echo "bench full failed rc=$?"; tail gpurun_out/bench_full.log; exit 1; }
+grep -h '"metric"' gpurun_out/bench_full.log
+head -12 gpurun_out/prof/run_kernel_stats.csv | cut -c1-200
+echo ALL_OK
