@@ -220,6 +220,17 @@ int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys,
 int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols,
                        const uint32_t *key_cols, const igx_pred *preds, uint32_t npreds,
                        uint64_t nrows, uint64_t base_idx);
+/* igx_groupby_update with two more inputs (either may be absent):
+ *   valid   (device u8, nullable): rows with 0 are skipped -- nil entries, or a mask from
+ *           igx_np_mark;
+ *   idx_col (IGX_NO_COL = row index + base_idx): a u64 column giving each row's global
+ *           event index.  Used to merge partial groups from other shards: key columns +
+ *           one u64 column per partial aggregate (summed by SUM aggregates) + their first
+ *           index, so first = min over shards (SURVEY.md §8(e) group-by exchange). */
+int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t ncols,
+                          const uint32_t *key_cols, const igx_pred *preds, uint32_t npreds,
+                          const uint8_t *valid, uint32_t idx_col, uint64_t nrows,
+                          uint64_t base_idx);
 /* Synchronises; fills the view; IGX_ENOSPC if capacity was exceeded. */
 int igx_groupby_finalize(igx_table *t, igx_table_view *view);
 /* Materialise groups idx[0..k) (device u32, e.g. igx_topk output) as packed rows of
@@ -236,6 +247,13 @@ int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uin
 int igx_groupby_destroy(igx_table *t);
 /* Diagnostics only (IGX_GB_DEBUG env bit 3): LDS-cache hits / misses since the last call. */
 int igx_groupby_debug_counts(igx_table *t, uint64_t *out4);
+
+/* ---- advise network-policy -------------------------------------------------------------- */
+/* keep[i] = 1 iff the advisor would consider event i (advisor.go:279-292): type == normal
+ * (0), pkt (PACKET_* code) is HOST (0) or OUTGOING (4), and not (HOST and hostip == raddr).
+ * typ/pkt/keep 4-byte aligned, hostip/raddr 16-byte aligned (device).  Asynchronous. */
+int igx_np_mark(igx_ctx *ctx, const uint8_t *typ, const uint8_t *pkt, const uint32_t *hostip,
+                const uint32_t *raddr, uint64_t nrows, uint8_t *keep);
 
 /* ---- log2 latency histograms ---------------------------------------------------------- */
 /* hist[(dev_index(dev)*ncont + cont) * nslots + slot] += 1 for every row with delta >= 0

@@ -97,12 +97,15 @@ SIGNATURES = [
                                 C.POINTER(_VP)]),
     ("igx_groupby_update", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(_U32), C.POINTER(Pred),
                                 _U32, _U64, _U64]),
+    ("igx_groupby_update_ex", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(_U32), C.POINTER(Pred),
+                                   _U32, _VP, _U32, _U64, _U64]),
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
     ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
     ("igx_groupby_reset", _I, [_VP]),
     ("igx_groupby_destroy", _I, [_VP]),
     ("igx_groupby_debug_counts", _I, [_VP, _VP]),
+    ("igx_np_mark", _I, [_VP, _VP, _VP, _VP, _VP, _U64, _VP]),
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
     ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),

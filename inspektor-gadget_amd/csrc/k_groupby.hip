@@ -79,7 +79,8 @@ struct GbArgs {
     uint32_t npred;
     uint32_t lds_entries;   // E (power of two)
     // input
-    const uint8_t *valid;
+    const uint8_t *valid;   // nullable: rows with 0 are skipped (nil / filtered entries)
+    const uint64_t *fidx;   // nullable: per-row global event index (merging partial groups)
     uint64_t n, base_idx;
     // table
     uint8_t *krec;          // key records
@@ -417,6 +418,10 @@ __device__ __forceinline__ int lds_adopt(const LdsCache<KW> &c, const uint32_t (
     return -1;
 }
 
+__device__ __forceinline__ uint64_t row_gidx(const GbArgs &a, uint64_t row) {
+    return a.fidx ? a.fidx[row] : a.base_idx + row;
+}
+
 __device__ __forceinline__ unsigned long long *rec_first(const GbArgs &a, uint32_t gs) {
     return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words);
 }
@@ -455,7 +460,7 @@ __device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::
         const uint64_t h = hash_key<KW>(k);
         uint32_t gs = SLOT_OVF;
         uint64_t first_ins = 0;
-        const uint64_t gidx = a.base_idx + row;
+        const uint64_t gidx = row_gidx(a, row);
         int slot = lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
         if (slot < 0) {
             gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
@@ -503,7 +508,7 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
                 uint32_t gs = SLOT_OVF;
                 const int slot = lds_lookup<KW>(c, k, h, gs);
                 if (a.dbg & 8u) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
-                if (slot >= 0) accumulate<KW>(a, c, slot, gs, v, a.base_idx + row, 0);
+                if (slot >= 0) accumulate<KW>(a, c, slot, gs, v, row_gidx(a, row), 0);
                 else miss = !(a.dbg & 2u);
             }
         }
@@ -833,6 +838,12 @@ static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
 
 extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
                                   const igx_pred *preds, uint32_t npreds, uint64_t nrows, uint64_t base_idx) {
+    return igx_groupby_update_ex(t, cols, ncols, key_cols, preds, npreds, nullptr, IGX_NO_COL, nrows, base_idx);
+}
+
+extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
+                                     const igx_pred *preds, uint32_t npreds, const uint8_t *valid, uint32_t idx_col,
+                                     uint64_t nrows, uint64_t base_idx) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     if (nrows == 0) return IGX_OK;
@@ -917,7 +928,13 @@ extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t nc
         a.pref[p] = r;
     }
     a.npred = npreds;
-    a.valid = nullptr;
+    a.valid = valid;
+    a.fidx = nullptr;
+    if (idx_col != IGX_NO_COL) {
+        if (idx_col >= ncols || cols[idx_col].width != 8)
+            return igx_fail(ctx, IGX_EINVAL, "groupby_update: index column must be a u64 column");
+        a.fidx = static_cast<const uint64_t *>(cols[idx_col].ptr);
+    }
     a.n = nrows;
     a.base_idx = base_idx;
     a.krec = t->krec;

@@ -77,7 +77,9 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
                 if (sdev[mid] < dv) lo = mid + 1; else hi = mid;
             }
             if (lo >= a.ndev || sdev[lo] != dv) continue;
-            const uint32_t key = sidx[lo] * a.ncont + (a.cont ? a.cont[row] : 0u);
+            const uint32_t ci = a.cont ? a.cont[row] : 0u;
+            if (ci >= a.ncont) continue;   // unknown container: not counted
+            const uint32_t key = sidx[lo] * a.ncont + ci;
             if (key - kbase >= a.Kp) continue;
             const int64_t d = a.delta[row];
             if (d < 0) continue;

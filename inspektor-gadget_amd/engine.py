@@ -155,14 +155,17 @@ class Table:
         self.naggs = len(aggs)
         self.capacity = capacity
 
-    def update(self, cols, key_cols, n, base_idx=0, preds=()):
+    def update(self, cols, key_cols, n, base_idx=0, preds=(), valid=None, idx_col=None):
+        """igx_groupby_update_ex: rows [0,n) of cols; valid (u8) masks rows out; idx_col is
+        the index of a u64 column of global event indices (merging partial groups)."""
         ctx = self.ctx
         ctx.bind_stream()
         ccols = (Col * len(cols))(*[col_of(t, dtype_kind(t)) for t in cols])
         kc = (C.c_uint32 * len(key_cols))(*key_cols)
         cp = (Pred * max(1, len(preds)))(*preds)
-        ctx.check(ctx.L.igx_groupby_update(self.h, ccols, len(cols), kc, cp, len(preds), n,
-                                           base_idx))
+        ctx.check(ctx.L.igx_groupby_update_ex(self.h, ccols, len(cols), kc, cp, len(preds),
+                                              ptr(valid), _abi.NO_COL if idx_col is None else idx_col,
+                                              n, base_idx))
 
     def reset(self):
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
@@ -236,6 +239,19 @@ def table_tensors(tab, fin):
             for i in range(tab.naggs)]
     first = rows[:, kb + 8 * tab.naggs:].contiguous().view(torch.uint64).flatten()
     return keys, aggs, first
+
+
+# ------------------------------------------------------------------------------------
+# advise network-policy
+# ------------------------------------------------------------------------------------
+def np_mark(typ, pkt, hostip, raddr):
+    """igx_np_mark: u8 keep mask of the advisor's event filter (advisor.go:279-292)."""
+    torch = torch_mod()
+    ctx = context()
+    n = typ.numel()
+    keep = torch.empty(max(4, (n + 3) // 4 * 4), dtype=torch.uint8, device=typ.device)
+    ctx.check(ctx.L.igx_np_mark(ctx.h, ptr(typ), ptr(pkt), ptr(hostip), ptr(raddr), n, ptr(keep)))
+    return keep[:n]
 
 
 # ------------------------------------------------------------------------------------

@@ -514,10 +514,11 @@ void or_hist_log2(const u32 *dev, const u32 *cont, const i64 *delta, u64 n, cons
         u32 di = 0;
         while (di < ndev && devs[di] != dev[i]) di++;
         if (di == ndev) continue;                    /* unknown device: not counted */
+        if (cont && cont[i] >= ncont) continue;      /* unknown container: not counted */
         u64 v = (u64)d / divisor;
         u64 slot = or_log2l(v);
         if (slot >= nslots) slot = nslots - 1;
-        u64 key = (u64)di * ncont + cont[i];
+        u64 key = (u64)di * ncont + (cont ? cont[i] : 0);
         hist[key * nslots + slot] += 1;
     }
 }

@@ -573,6 +573,27 @@ def gen_file(seed, rank, G, cdf, base, n):
     return o
 
 
+def np_mark(ev):
+    """advisor.go:279-292 on the encoded C4 stream: type normal (0), pkt HOST (0) or
+    OUTGOING (4), and not (HOST and PodHostIP == RemoteAddr)."""
+    t, p = ev["type"], ev["pkt"]
+    return (t == 0) & ((p == 0) | (p == 4)) & ~((p == 0) & (ev["hostip"] == ev["raddr"]))
+
+
+def pad_keys(batch, names):
+    """pack_cols with every column padded to 4 bytes (the device's packed key layout)."""
+    parts = []
+    for nm in names:
+        a = np.ascontiguousarray(batch[nm])
+        n = a.shape[0]
+        b = a.view(np.uint8).reshape(n, -1)
+        w = b.shape[1]
+        if w % 4:
+            b = np.concatenate([b, np.zeros((n, 4 - w % 4), np.uint8)], axis=1)
+        parts.append(b)
+    return np.concatenate(parts, axis=1)
+
+
 TCP_KEY_COLS = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family")
 
 

@@ -192,3 +192,8 @@ def test_hist_log2_c3(oracle, E, H, torch):
     got1 = H.host(E.hist_log2(ev["dev"], None, ev["delta"].view(torch.int64), devs[:1], 1))
     ref1 = oracle.hist_log2(ev_h["dev"], np.zeros(n, np.uint32), ev_h["delta"], devs[:1], 1)
     assert np.array_equal(got1, ref1)
+    # containers outside [0, ncont) and devices outside devs are not counted; ms divisor
+    got2 = H.host(E.hist_log2(ev["dev"], ev["cont"], ev["delta"].view(torch.int64), devs[3:9], 100,
+                              divisor=1_000_000))
+    ref2 = oracle.hist_log2(ev_h["dev"], ev_h["cont"], ev_h["delta"], devs[3:9], 100, divisor=1_000_000)
+    assert np.array_equal(got2, ref2)
