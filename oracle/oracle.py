@@ -697,3 +697,142 @@ def _flatten(vals, sum_cols):
                     s -= 1 << (8 * w)
                 base[name] = s
     return base
+
+
+# ------------------------------------------------------------------------------------------
+# advise network-policy (pkg/gadgets/advise/networkpolicy/advisor/advisor.go) -- a direct
+# restatement over parsed JSON events, event by event, with Python dicts in place of Go maps.
+# ------------------------------------------------------------------------------------------
+ADVISOR_IGNORE = {"controller-revision-hash", "pod-template-generation", "pod-template-hash"}
+
+
+def _adv_keys(labels):                                   # labelFilteredKeyList :104-116
+    return sorted(k for k in (labels or {}) if k not in ADVISOR_IGNORE)
+
+
+def _adv_filter(labels):                                 # labelFilter :118-127
+    return {k: v for k, v in (labels or {}).items() if k not in ADVISOR_IGNORE}
+
+
+def _adv_keystr(labels):                                 # labelKeyString :132-141
+    return ",".join("%s=%s" % (k, labels[k]) for k in _adv_keys(labels))
+
+
+def _adv_peer_key(e):                                    # networkPeerKey :150-160
+    k = e.get("remoteKind", "")
+    if k in ("pod", "svc"):
+        r = k + ":" + e.get("remoteNamespace", "") + ":" + _adv_keystr(e.get("remoteLabels"))
+    elif k == "other":
+        r = k + ":" + e.get("remoteAddr", "")
+    else:
+        r = ""
+    return "%s:%d" % (r, int(e.get("port", 0)))
+
+
+def _adv_rule(e):                                        # eventToRule :162-216
+    ports = [{"port": int(e.get("port", 0)), "protocol": e.get("proto", "").upper()}]
+    k = e.get("remoteKind", "")
+    if k in ("pod", "svc"):
+        lab = _adv_filter(e.get("remoteLabels")) if k == "pod" else dict(e.get("remoteLabels") or {})
+        peer = {"podSelector": ({"matchLabels": lab} if lab else {})}
+        if e.get("namespace", "") != e.get("remoteNamespace", ""):
+            peer["namespaceSelector"] = {"matchLabels": {"kubernetes.io/metadata.name":
+                                                         e.get("remoteNamespace", "")}}
+        return ports, [peer]
+    if k == "other":
+        a = e.get("remoteAddr", "")
+        return ports, ([] if a == "127.0.0.1" else [{"ipBlock": {"cidr": a + "/32"}}])
+    raise ValueError("unknown event")
+
+
+def _yaml_scalar(v):
+    import re as _re
+    if v is None:
+        return "null"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    s = str(v)
+    if s == "":
+        return '""'
+    if _re.fullmatch(r"[-+]?\d+(\.\d*)?([eE][-+]?\d+)?|true|false|null|~|yes|no|on|off|y|n", s, _re.I):
+        return '"%s"' % s
+    if _re.fullmatch(r"[A-Za-z0-9_./][A-Za-z0-9_./ -]*", s) and not s.endswith(" "):
+        return s
+    return "'" + s.replace("'", "''") + "'"
+
+
+def yaml_text(v, ind=0):
+    """go-yaml v2 block style as sigs.k8s.io/yaml emits it: sorted keys, sequences at
+    their key's indentation, {} / [] for empty collections."""
+    lines = []
+    p = " " * ind
+
+    def leaf(x):
+        return "{}" if isinstance(x, dict) else ("[]" if isinstance(x, list) else _yaml_scalar(x))
+    if isinstance(v, dict):
+        for k in sorted(v):
+            x = v[k]
+            if isinstance(x, dict) and x:
+                lines.append("%s%s:" % (p, k))
+                lines.append(yaml_text(x, ind + 2).rstrip("\n"))
+            elif isinstance(x, list) and x:
+                lines.append("%s%s:" % (p, k))
+                lines.append(yaml_text(x, ind).rstrip("\n"))
+            else:
+                lines.append("%s%s: %s" % (p, k, leaf(x)))
+    else:
+        for x in v:
+            if isinstance(x, (dict, list)) and x:
+                body = yaml_text(x, ind + 2).rstrip("\n")
+                lines.append(p + "- " + body[ind + 2:])
+            else:
+                lines.append("%s- %s" % (p, leaf(x)))
+    return "\n".join(lines) + "\n"
+
+
+def advisor_policies(events):
+    """GeneratePolicies (:277-372).  Sources are visited in first-occurrence order and the
+    final name sort is stable (Go's map order + sort.Slice leave equal names unordered)."""
+    by_src = {}
+    for e in events:                                     # :279-300
+        if e.get("type") != "normal":
+            continue
+        pk = e.get("pktType", "")
+        if pk not in ("HOST", "OUTGOING"):
+            continue
+        if pk == "HOST" and e.get("podHostIP", "") == e.get("remoteAddr", ""):
+            continue
+        key = e.get("namespace", "") + ":" + _adv_keystr(e.get("podLabels"))
+        by_src.setdefault(key, []).append(e)
+    out = []
+    for evs in by_src.values():
+        egress, ingress = {}, {}
+        for e in evs:                                    # :302-320 first event wins
+            k = _adv_peer_key(e)
+            d = egress if e.get("pktType") == "OUTGOING" else ingress
+            if k not in d:
+                d[k] = e
+        def rules(d, field):
+            r = []
+            for e in d.values():
+                ports, peers = _adv_rule(e)
+                if peers:
+                    r.append({"ports": ports, field: peers})
+            return sorted(r, key=lambda x: (x["ports"][0]["protocol"], x["ports"][0]["port"], yaml_text(x)))
+        e0 = evs[0]
+        name = (e0.get("podOwner") or e0.get("pod", "")) + "-network"
+        lab = _adv_filter(e0.get("podLabels"))
+        spec = {"podSelector": ({"matchLabels": lab} if lab else {}), "policyTypes": ["Ingress", "Egress"]}
+        ing, egr = rules(ingress, "from"), rules(egress, "to")
+        if ing:
+            spec["ingress"] = ing
+        if egr:
+            spec["egress"] = egr
+        out.append({"apiVersion": "networking.k8s.io/v1", "kind": "NetworkPolicy",
+                    "metadata": {"creationTimestamp": None, "name": name,
+                                 "namespace": e0.get("namespace", "")},
+                    "spec": spec, "status": {}})
+    out.sort(key=lambda p: p["metadata"]["name"])
+    return out

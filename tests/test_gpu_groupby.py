@@ -222,3 +222,55 @@ def test_table_sort_and_gather(oracle, E, H, igx, torch):
             g16 = rows[:, 12:20].copy().view(np.uint64).ravel()   # key_bytes = 12 (4+4+4 padded)
             assert int(g16.max()) < (1 << 16)
     tab.destroy()
+
+
+def test_netpolicy_mark_and_masked_distinct(oracle, E, H, igx, torch):
+    """igx_np_mark (advisor.go:279-292) + distinct over the kept rows (valid mask)."""
+    A = igx._abi
+    n = 400_003                      # ragged tail for the 4-rows-per-thread mark kernel
+    ev_h = oracle.gen_np(0xC4, 3_000, 30_000, 17, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
+    ref_keep = oracle.np_mark(ev_h)
+    assert np.array_equal(H.host(keep).astype(bool), ref_keep)
+    names = ("src", "pkt", "peer", "port")
+    tab = E.Table([4, 1, 4, 2], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], n)
+    tab.update([ev[k] for k in names], [0, 1, 2, 3], n, 17, valid=keep)
+    o = oracle.groupby(oracle.pack_cols(ev_h, names), [{"kind": "count"}], valid=ref_keep, base_idx=17)
+    _check(E, H, tab, [4, 1, 4, 2], *o)
+    tab.destroy()
+
+
+def test_merge_partials_on_device(oracle, E, H, igx, torch):
+    """Owner-side merge of partial groups (igx_groupby_update_ex with an index column): three
+    shards aggregated separately, their gathered rows merged == one aggregation of all."""
+    A = igx._abi
+    D = igx.dist
+    n, G = 300_000, 5_000
+    ev_h = oracle.gen_file(0xC5, 0, G, oracle.zipf_cdf(G, 1.05), 0, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    names = ("inode", "dev", "pid", "tid", "op", "count")
+    widths = [8, 4, 4, 4]
+    aggs = [A.Agg(A.AGG_COUNT, 0, 4, 8, 1), A.Agg(A.AGG_SUM, 5, 4, 4, 1)]
+    rows = []
+    cuts = [0, 70_001, 190_000, n]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        t = E.Table(widths, aggs, 2 * G)
+        t.update([ev[k][a:b] for k in names], [0, 1, 2, 3], b - a, a)
+        fin = t.finalize()
+        slots = t.sort([(A.TSRC_FIRST, 0, False)], 0)
+        rows.append(t.gather(slots))
+        t.destroy()
+    allrows = torch.cat(rows)
+    tab = D.merge_partials(allrows, widths, [8, 4], 2 * G)
+    o = oracle.groupby(oracle.pack_cols(ev_h, names[:4]),
+                       [{"kind": "count", "cond": ev_h["op"], "cond_val": 1},
+                        {"kind": "sum", "val": ev_h["count"], "cond": ev_h["op"], "cond_val": 1,
+                         "out_width": 4}])
+    _check(E, H, tab, widths, *o)
+    # the merged table's top-K equals the single-pass one (wbytes DESC)
+    slots = tab.sort([(A.TSRC_AGG, 1, True)], 20)
+    got_first = H.host(tab.gather(slots))[:, -8:].copy().view(np.uint64).ravel()
+    perm = oracle.go_sort_entries([(o[1][1].astype(np.uint32), "uint32", True)], len(o[0]))
+    assert np.array_equal(got_first, o[2][perm.astype(np.int64)][:20])
+    tab.destroy()
