@@ -70,7 +70,11 @@ enum igx_kind {
 };
 
 enum igx_cmp { IGX_CMP_EQ = 0, IGX_CMP_REGEX = 1, IGX_CMP_LT = 2, IGX_CMP_LE = 3,
-               IGX_CMP_GT = 4, IGX_CMP_GE = 5 };
+               IGX_CMP_GT = 4, IGX_CMP_GE = 5,
+               /* group-by predicates only (a BPF probe's set test, e.g. tcptop.bpf.c:54
+                * `family != AF_INET && family != AF_INET6` -> drop): the field equals one
+                * of the ref_len / width values packed in ref (at most 8 bytes) */
+               IGX_CMP_IN = 6 };
 
 #define IGX_COL_VIRTUAL 1u   /* columns.AddColumn virtual column (columns.go:282-309) */
 #define IGX_COL_EXTRACTOR 2u /* column with SetExtractor (columns.go:320-332) */
@@ -175,6 +179,9 @@ typedef struct {
     uint32_t cond_col;  /* IGX_NO_COL or column whose value must equal cond_val */
     uint32_t out_width; /* result wraps to this many bytes (1,2,4,8) */
     uint64_t cond_val;
+    uint64_t divisor;   /* SUM of an unsigned column: add value / divisor per event (0, 1 =
+                         * plain sum), e.g. biotop's `us += delta_ns / 1000`
+                         * (pkg/gadgets/top/block-io/tracer/bpf/biotop.bpf.c:98,119) */
 } igx_agg;
 
 /* The table is an open-addressing array of n_slots slots; a group's id is its slot.
@@ -199,7 +206,10 @@ typedef struct {
 } igx_table_view;
 
 /* Sort key over a table's columns (igx_groupby_sort). */
-enum igx_tsrc { IGX_TSRC_AGG = 0, IGX_TSRC_FIRST = 1, IGX_TSRC_KEY = 2 };
+/* IGX_TSRC_CONST: a column that holds the same value for every group (e.g. the
+ * CommonData enrichment strings when nothing enriches).  Go still runs a SliceStable pass
+ * for it, so it orders nothing but its '-' flips the tie parity. */
+enum igx_tsrc { IGX_TSRC_AGG = 0, IGX_TSRC_FIRST = 1, IGX_TSRC_KEY = 2, IGX_TSRC_CONST = 3 };
 typedef struct {
     uint32_t src;    /* enum igx_tsrc */
     uint32_t index;  /* aggregate index (IGX_TSRC_AGG) */
@@ -259,7 +269,9 @@ int igx_np_mark(igx_ctx *ctx, const uint8_t *typ, const uint8_t *pkt, const uint
 /* hist[(dev_index(dev)*ncont + cont) * nslots + slot] += 1 for every row with delta >= 0
  * (delta is s64 ns), slot = min(log2l(delta/divisor), nslots-1).  devs (host, ndev <= 64)
  * lists the device numbers (dev_index = position); rows with other devs are ignored.
- * cont may be NULL (ncont must then be 1).  hist (device u32) accumulates.  Async. */
+ * ndev == 0 is the shipped gadget's keying (no targ_per_disk / targ_per_flag): every row
+ * is device index 0 and dev may be NULL.  cont may be NULL (ncont must then be 1).
+ * hist (device u32, max(ndev,1)*ncont*nslots) accumulates.  Async. */
 int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                   const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
                   uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);

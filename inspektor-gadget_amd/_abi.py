@@ -18,7 +18,7 @@ IGX_ENOSPC = -28
 IGX_ENOTSUP = -95
 
 KIND_INT, KIND_UINT, KIND_FLOAT, KIND_BYTES, KIND_BOOL, KIND_OTHER = range(6)
-CMP_EQ, CMP_REGEX, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
+CMP_EQ, CMP_REGEX, CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_IN = range(7)
 COL_VIRTUAL, COL_EXTRACTOR = 1, 2
 NO_COL = 0xFFFFFFFF
 MAX_REF = 256
@@ -46,7 +46,7 @@ class SortKey(C.Structure):
 
 class Agg(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("col", C.c_uint32), ("cond_col", C.c_uint32),
-                ("out_width", C.c_uint32), ("cond_val", C.c_uint64)]
+                ("out_width", C.c_uint32), ("cond_val", C.c_uint64), ("divisor", C.c_uint64)]
 
 
 class TableView(C.Structure):
@@ -57,7 +57,7 @@ class TableView(C.Structure):
                 ("d_n_groups", C.c_void_p)]
 
 
-TSRC_AGG, TSRC_FIRST, TSRC_KEY = 0, 1, 2
+TSRC_AGG, TSRC_FIRST, TSRC_KEY, TSRC_CONST = 0, 1, 2, 3
 
 
 class TSortKey(C.Structure):

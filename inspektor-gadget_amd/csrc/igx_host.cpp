@@ -413,6 +413,7 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
         const igx_pred &p = preds[i];
         if (p.col >= ncols) return igx_fail(ctx, IGX_EINVAL, "predicate column %u out of range", p.col);
         if (p.cmp == IGX_CMP_REGEX) return igx_fail(ctx, IGX_ENOTSUP, "regular-expression filters run on the host");
+        if (p.cmp > IGX_CMP_GE) return igx_fail(ctx, IGX_EINVAL, "filter: comparison %u is not a FilterSpec", p.cmp);
         const igx_col &c = cols[p.col];
         DevPred &d = out->p[i];
         d.ptr = static_cast<const uint8_t *>(c.ptr);
@@ -485,6 +486,10 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
     for (uint32_t i = 0; i < nkeys; ++i) {
         const igx_sortkey &k = keys[i];
         if (k.kind == IGX_KIND_BOOL || k.kind == IGX_KIND_OTHER) continue;   // sort.go:77-78
+        if (k.width == 0) {   // constant column: a pass that orders nothing, parity only
+            parity ^= k.desc ? 1u : 0u;
+            continue;
+        }
         SortPlanKey p{};
         p.ptr = static_cast<const uint8_t *>(k.ptr);
         p.width = k.width;
@@ -534,6 +539,6 @@ extern "C" int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *
                              uint64_t nrows, const uint32_t *devs, uint32_t ndev, uint32_t ncont,
                              uint64_t divisor, uint32_t nslots, uint32_t *hist) {
     if (!ctx) return IGX_EINVAL;
-    if (nrows && (!dev || !delta || !hist || !devs)) return igx_fail(ctx, IGX_EINVAL, "hist: null argument");
+    if (nrows && (!delta || !hist || (ndev && (!dev || !devs)))) return igx_fail(ctx, IGX_EINVAL, "hist: null argument");
     return launch_hist_log2(ctx, dev, cont, delta, nrows, devs, ndev, ncont, divisor, nslots, hist);
 }

@@ -70,12 +70,13 @@ struct GbArgs {
     const uint8_t *vptr[AMAX];
     const uint8_t *cptr[AMAX];
     uint64_t cval[AMAX];
+    uint64_t vdiv[AMAX];    // 0: plain value, else value / vdiv (unsigned)
     uint32_t vwidth[AMAX], vsign[AMAX], vcount[AMAX], cwidth[AMAX], hascond[AMAX];
     uint32_t naggs;
     // scalar predicates (FilterSpec on a <= 8-byte column), AND-ed
     const uint8_t *pptr[PMAX];
     uint64_t pref[PMAX];
-    uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX];
+    uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
     uint32_t npred;
     uint32_t lds_entries;   // E (power of two)
     // input
@@ -201,7 +202,13 @@ struct GenericLayout {
 // FilterSpec on a scalar column, evaluated on an already loaded value
 // (getComparisonFuncForComparisonType, filter.go:236-263: (field OP ref) != negate).
 __device__ __forceinline__ bool pred_scalar(uint64_t v, uint64_t ref, uint32_t width, uint32_t kind,
-                                            uint32_t cmp, uint32_t neg) {
+                                            uint32_t cmp, uint32_t neg, uint32_t cnt) {
+    if (cmp == IGX_CMP_IN) {   // set membership: cnt values of `width` bytes packed in ref
+        const uint64_t m = width >= 8 ? ~0ull : ((1ull << (8 * width)) - 1);
+        bool in = false;
+        for (uint32_t i = 0; i < cnt; ++i) in = in || v == ((ref >> (8 * width * i)) & m);
+        return in != (neg != 0);
+    }
     int c;
     if (kind == IGX_KIND_FLOAT) {
         double x, y;
@@ -363,11 +370,13 @@ __device__ __forceinline__ bool load_row(const GbArgs &a, uint64_t row, uint32_t
     bool ok = vb != 0;
 #pragma unroll
     for (int p = 0; p < PMAX; ++p)
-        if (p < (int)a.npred) ok = ok && pred_scalar(pv[p], a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p]);
+        if (p < (int)a.npred) ok = ok && pred_scalar(pv[p], a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p],
+                                     a.pcnt[p]);
 #pragma unroll
     for (int x = 0; x < AMAX; ++x) {
         if (x < (int)a.naggs) {
             uint64_t val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(v[x], a.vwidth[x]) : v[x]);
+            if (a.vdiv[x]) val /= a.vdiv[x];
             if (a.hascond[x] && cv[x] != a.cval[x]) val = 0;
             v[x] = val;
         } else {
@@ -702,6 +711,7 @@ struct igx_table {
 using TcpKey = StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>;   // ip_key_t (tcptop.h:8-17)
 using FileKey = StaticLayout<8, 4, 4, 4>;                 // file_id (filetop.h:13-18)
 using NetPolicyKey = StaticLayout<4, 1, 4, 2>;            // (src, direction, peer, port)
+using BioKey = StaticLayout<8, 4, 4, 4, 4, 16>;           // info_t (biotop.h:24-32)
 
 template <class L>
 static bool layout_is(const uint32_t *widths, uint32_t nkeys) {
@@ -722,6 +732,7 @@ static int static_kw(const uint32_t *w, uint32_t n) {
     if (layout_is<TcpKey>(w, n)) return TcpKey::KW;
     if (layout_is<FileKey>(w, n)) return FileKey::KW;
     if (layout_is<NetPolicyKey>(w, n)) return NetPolicyKey::KW;
+    if (layout_is<BioKey>(w, n)) return BioKey::KW;
     if (n == 1 && (w[0] == 1 || w[0] == 2 || w[0] == 4 || w[0] == 8 || w[0] == 16)) return (int)((w[0] + 3) / 4);
     return 0;
 }
@@ -894,6 +905,11 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
                 return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: agg width %u", a.vwidth[x]);
             if (cols[g.col].kind == IGX_KIND_FLOAT)
                 return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: float sums are not supported");
+            if (g.divisor > 1) {
+                if (a.vsign[x])
+                    return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: divisor on a signed column");
+                a.vdiv[x] = g.divisor;
+            }
         }
         a.cptr[x] = dummy;
         a.cwidth[x] = 1;
@@ -918,13 +934,22 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
             (c.kind == IGX_KIND_FLOAT && c.width < 4))
             return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: predicate %u is not a scalar comparison "
                                               "(run igx_filter first)", p);
+        if (q.cmp == IGX_CMP_IN) {
+            if (q.ref_len == 0 || q.ref_len % c.width || q.ref_len > 8 || c.kind == IGX_KIND_FLOAT)
+                return igx_fail(ctx, IGX_EINVAL, "groupby_update: IN predicate %u needs 1..8/width "
+                                                 "integer values", p);
+            a.pcnt[p] = q.ref_len / c.width;
+        } else if (q.cmp > IGX_CMP_GE) {
+            return igx_fail(ctx, IGX_EINVAL, "groupby_update: predicate %u comparison %u", p, q.cmp);
+        }
         a.pptr[p] = static_cast<const uint8_t *>(c.ptr);
         a.pwidth[p] = c.width;
         a.pkind[p] = c.kind;
         a.pcmp[p] = q.cmp;
         a.pneg[p] = q.negate;
         uint64_t r = 0;
-        for (uint32_t b = 0; b < c.width; ++b) r |= (uint64_t)q.ref[b] << (8 * b);
+        const uint32_t nb = q.cmp == IGX_CMP_IN ? q.ref_len : c.width;
+        for (uint32_t b = 0; b < nb; ++b) r |= (uint64_t)q.ref[b] << (8 * b);
         a.pref[p] = r;
     }
     a.npred = npreds;
@@ -966,6 +991,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     else if (layout_is<FileKey>(kw, t->nkeys)) launch_gb<FileKey>(ctx, a, blocks);
     else if (layout_is<NetPolicyKey>(kw, t->nkeys))
         launch_gb<NetPolicyKey>(ctx, a, blocks);
+    else if (layout_is<BioKey>(kw, t->nkeys)) launch_gb<BioKey>(ctx, a, blocks);
     else if (t->nkeys == 1 && kw[0] == 1) launch_gb<StaticLayout<1>>(ctx, a, blocks);
     else if (t->nkeys == 1 && kw[0] == 2) launch_gb<StaticLayout<2>>(ctx, a, blocks);
     else if (t->nkeys == 1 && kw[0] == 4) launch_gb<StaticLayout<4>>(ctx, a, blocks);
@@ -1062,6 +1088,10 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
             sk[i].ptr = t->vrec;
             sk[i].width = 8;
             sk[i].kind = IGX_KIND_UINT;
+        } else if (q.src == IGX_TSRC_CONST) {
+            sk[i].ptr = t->vrec;   // never read: width 0 marks a parity-only pass
+            sk[i].width = 0;
+            sk[i].kind = IGX_KIND_BYTES;
         } else if (q.src == IGX_TSRC_KEY) {
             if (q.offset + q.width > t->key_words * 4)
                 return igx_fail(ctx, IGX_EINVAL, "groupby_sort: key bytes out of range");

@@ -5,15 +5,22 @@
 //   v = delta / 1000 (usecs; 1e6 with targ_ms);  slot = log2l(v) (bits.bpf.h:8-29) clamped
 //   to MAX_SLOTS-1 = 26;  __sync_fetch_and_add(&slots[slot], 1) (u32).
 // log2l(v) == floor(log2 v) for v >= 1 and 0 for v == 0, i.e. 63 - clz64(v).
-// The reference keys the histogram by hist_key{cmd_flags, dev}; C3 keys it by
-// (dev, container) -- dense key = dev_index * ncont + cont.
+// The reference keys the histogram by hist_key{cmd_flags, dev}; the shipped gadget sets
+// neither targ_per_disk nor targ_per_flag, so every event lands in key {0,0} (ndev == 0
+// here).  C3 keys it by (dev, container): dense key = dev_index * ncont + cont.
 //
-// Layout: hist is [nkeys][nslots] u32 in HBM.  Each workgroup privatises a slice of it
-// in LDS (u32 counters, up to 120 KB); when the whole histogram does not fit, the key
-// space is split into P partitions and P workgroups that share an XCD (blockIdx % 8,
-// speed only) sweep the same input chunks, each counting its own partition -- the
-// repeated reads are L2 hits.  Small histograms are replicated per wave to spread LDS
-// atomic contention.  Commit: one coalesced HBM atomic add per non-zero bin per WG.
+// Layout: hist is [nkeys][nslots] u32 in HBM.  Each workgroup privatises a key partition
+// of it in LDS as 16-bit counters (two per dword, bumped with 32-bit LDS atomics).  Exact
+// by construction: rows are consumed in tiles of at most 32768 per workgroup with a
+// barrier between tiles, and the one lane whose add takes a counter from 0x7FFF to 0x8000
+// moves 0x8000 to HBM (LDS subtract + HBM add) before that barrier.  So every counter is
+// below 0x8000 when a tile starts, gains at most 0x8000 during it and never carries into
+// its neighbour.  u16 halves the LDS footprint: C3's 4096 keys x 27 slots need two
+// partitions instead of four.  The partitions of a key range run on blocks that share an
+// XCD (blockIdx % 8, speed only) and sweep the same chunks, so the repeated reads are L2
+// hits.  Each lane keeps 8 rows (128 B of loads) in flight per chunk -- the kernel is
+// bound by bytes in flight, not by arithmetic.  Small histograms are replicated per wave
+// to spread LDS atomic contention.  Commit: one HBM atomic add per non-zero counter.
 #include <algorithm>
 #include <vector>
 
@@ -22,80 +29,148 @@
 namespace {
 
 constexpr int TB = 1024;
-constexpr uint32_t LDS_BUDGET = 120 * 1024;
-constexpr uint64_t CHUNK = 1 << 16;   // rows per chunk
+constexpr int RPL = 8;                                  // rows per lane per chunk
+constexpr uint64_t CHUNK = (uint64_t)TB * RPL;          // 8192 rows
+constexpr int CHUNKS_PER_TILE = 4;                      // 32768 rows between barriers
+constexpr uint32_t LDS_BUDGET = 144 * 1024;
+constexpr uint32_t DEVTAB = 256;                        // LDS hash of device numbers
 
 struct HistArgs {
     const uint32_t *dev;
     const uint32_t *cont;
     const int64_t *delta;
     uint64_t n;
-    uint32_t devs_sorted[64];
-    uint32_t devs_index[64];
+    uint32_t dev_key[DEVTAB];   // open-addressed dev -> index (0xFFFFFFFF = empty)
+    uint8_t dev_idx[DEVTAB];
+    uint32_t single;            // ndev == 0: every row is device 0 (the shipped gadget)
     uint32_t ndev, ncont, nslots;
-    uint32_t P;          // key partitions
-    uint32_t Kp;         // keys per partition
-    uint32_t R;          // LDS replicas
-    uint32_t ngroups;    // chunk groups (multiple of 8)
+    uint32_t P;                 // key partitions
+    uint32_t Kp;                // keys per partition
+    uint32_t R;                 // LDS replicas
+    uint32_t rep_words;         // dwords per replica (two u16 counters each)
+    uint32_t ngroups;           // chunk groups (multiple of 8)
     uint64_t divisor;
     uint32_t *hist;
 };
+
+__host__ __device__ __forceinline__ uint32_t dev_hash(uint32_t d) { return (d * 0x9E3779B1u) >> 24; }
 
 template <int DIV>
 __device__ __forceinline__ uint64_t divide(uint64_t v, uint64_t d) {
     if constexpr (DIV == 1000) return v / 1000ull;
     else if constexpr (DIV == 1000000) return v / 1000000ull;
+    else if constexpr (DIV == 1) return v;
     else return v / d;
 }
 
 template <int DIV>
+struct Counter {
+    const HistArgs &a;
+    const uint32_t *skey;
+    const uint8_t *sidx;
+    uint32_t *hr;
+    uint32_t kbase;
+
+    __device__ __forceinline__ void operator()(uint32_t dv, uint32_t ci, int64_t d) const {
+        uint32_t di = 0;
+        if (!a.single) {
+            uint32_t e = dev_hash(dv);
+            uint32_t k;
+            while ((k = skey[e]) != dv && k != 0xFFFFFFFFu) e = (e + 1) & (DEVTAB - 1);
+            if (k != dv) return;   // unknown device: not counted
+            di = sidx[e];
+        }
+        if (ci >= a.ncont) return;   // unknown container: not counted
+        if (d < 0) return;
+        const uint32_t kk = di * a.ncont + ci - kbase;
+        if (kk >= a.Kp) return;      // another partition's key
+        const uint64_t v = divide<DIV>((uint64_t)d, a.divisor);
+        uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
+        slot = min(slot, a.nslots - 1);
+        const uint32_t idx = kk * a.nslots + slot;
+        const uint32_t sh = (idx & 1u) * 16u;
+        const uint32_t old = atomicAdd(&hr[idx >> 1], 1u << sh);
+        if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {   // this add took it to 0x8000
+            atomicSub(&hr[idx >> 1], 0x8000u << sh);
+            atomicAdd(&a.hist[(uint64_t)kbase * a.nslots + idx], 0x8000u);
+        }
+    }
+};
+
+template <int DIV, bool VEC>
 __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     extern __shared__ uint32_t h[];
-    const uint32_t part_bins = a.Kp * a.nslots;
-    for (uint32_t i = threadIdx.x; i < part_bins * a.R; i += TB) h[i] = 0;
-    __shared__ uint32_t sdev[64], sidx[64];
-    if (threadIdx.x < 64) {
-        sdev[threadIdx.x] = a.devs_sorted[threadIdx.x];
-        sidx[threadIdx.x] = a.devs_index[threadIdx.x];
+    __shared__ uint32_t skey[DEVTAB];
+    __shared__ uint8_t sidx[DEVTAB];
+    for (uint32_t i = threadIdx.x; i < a.rep_words * a.R; i += TB) h[i] = 0;
+    if (threadIdx.x < DEVTAB) {
+        skey[threadIdx.x] = a.dev_key[threadIdx.x];
+        sidx[threadIdx.x] = a.dev_idx[threadIdx.x];
     }
     __syncthreads();
     const uint32_t b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const uint32_t p = j % a.P, g = j / a.P;
     const uint32_t cgroup = g * 8 + xcd;
-    const uint32_t kbase = p * a.Kp;
-    const uint32_t rep = (threadIdx.x >> 6) % a.R;
-    uint32_t *hr = h + rep * part_bins;
+    const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp};
     const uint64_t nchunks = (a.n + CHUNK - 1) / CHUNK;
+    uint32_t it = 0;
     for (uint64_t c = cgroup; c < nchunks; c += a.ngroups) {
-        const uint64_t end = min(a.n, (c + 1) * CHUNK);
-        for (uint64_t row = c * CHUNK + threadIdx.x; row < end; row += TB) {
-            const uint32_t dv = a.dev[row];
-            // binary search in the sorted device table
-            uint32_t lo = 0, hi = a.ndev;
-            while (lo < hi) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (sdev[mid] < dv) lo = mid + 1; else hi = mid;
+        const uint64_t base = c * CHUNK;
+        if (VEC && base + CHUNK <= a.n) {
+            // lane t covers rows base + 4t .. +3 and base + 4096 + 4t .. +3: every load is
+            // 16 B and a wave's loads are contiguous
+            const uint64_t r0 = base + 4ull * threadIdx.x, r1 = r0 + 4ull * TB;
+            const uint4 dv0 = *reinterpret_cast<const uint4 *>(a.dev + r0);
+            const uint4 dv1 = *reinterpret_cast<const uint4 *>(a.dev + r1);
+            uint4 ci0 = make_uint4(0, 0, 0, 0), ci1 = ci0;
+            if (a.cont) {
+                ci0 = *reinterpret_cast<const uint4 *>(a.cont + r0);
+                ci1 = *reinterpret_cast<const uint4 *>(a.cont + r1);
             }
-            if (lo >= a.ndev || sdev[lo] != dv) continue;
-            const uint32_t ci = a.cont ? a.cont[row] : 0u;
-            if (ci >= a.ncont) continue;   // unknown container: not counted
-            const uint32_t key = sidx[lo] * a.ncont + ci;
-            if (key - kbase >= a.Kp) continue;
-            const int64_t d = a.delta[row];
-            if (d < 0) continue;
-            const uint64_t v = divide<DIV>((uint64_t)d, a.divisor);
-            uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
-            slot = min(slot, a.nslots - 1);
-            atomicAdd(&hr[(key - kbase) * a.nslots + slot], 1u);
+            const longlong2 d0 = *reinterpret_cast<const longlong2 *>(a.delta + r0);
+            const longlong2 d1 = *reinterpret_cast<const longlong2 *>(a.delta + r0 + 2);
+            const longlong2 d2 = *reinterpret_cast<const longlong2 *>(a.delta + r1);
+            const longlong2 d3 = *reinterpret_cast<const longlong2 *>(a.delta + r1 + 2);
+            count(dv0.x, ci0.x, d0.x);
+            count(dv0.y, ci0.y, d0.y);
+            count(dv0.z, ci0.z, d1.x);
+            count(dv0.w, ci0.w, d1.y);
+            count(dv1.x, ci1.x, d2.x);
+            count(dv1.y, ci1.y, d2.y);
+            count(dv1.z, ci1.z, d3.x);
+            count(dv1.w, ci1.w, d3.y);
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const uint64_t row = base + (uint64_t)r * TB + threadIdx.x;
+                if (row < a.n) count(a.dev ? a.dev[row] : 0u, a.cont ? a.cont[row] : 0u, a.delta[row]);
+            }
         }
+        if (++it % CHUNKS_PER_TILE == 0) __syncthreads();   // tile boundary (see header)
     }
     __syncthreads();
-    const uint32_t nkeys_here = min(a.Kp, a.ndev * a.ncont - min(kbase, a.ndev * a.ncont));
+    const uint32_t nkeys = a.ndev * a.ncont;
+    const uint32_t kbase = p * a.Kp;
+    const uint32_t nkeys_here = kbase < nkeys ? min(a.Kp, nkeys - kbase) : 0u;
     for (uint32_t i = threadIdx.x; i < nkeys_here * a.nslots; i += TB) {
         uint32_t s = 0;
-        for (uint32_t r = 0; r < a.R; ++r) s += h[r * part_bins + i];
+        for (uint32_t r = 0; r < a.R; ++r) s += (h[r * a.rep_words + (i >> 1)] >> ((i & 1u) * 16u)) & 0xFFFFu;
         if (s) atomicAdd(&a.hist[(uint64_t)kbase * a.nslots + i], s);
     }
+}
+
+template <int DIV>
+void launch(const HistArgs &a, uint32_t blocks, size_t lds, hipStream_t s, bool vec) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist<DIV, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist<DIV, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
+        attr_set = true;
+    }
+    if (vec) hipLaunchKernelGGL((k_hist<DIV, true>), dim3(blocks), dim3(TB), lds, s, a);
+    else hipLaunchKernelGGL((k_hist<DIV, false>), dim3(blocks), dim3(TB), lds, s, a);
 }
 
 }  // namespace
@@ -104,57 +179,55 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
                      uint64_t nrows, const uint32_t *devs, uint32_t ndev, uint32_t ncont,
                      uint64_t divisor, uint32_t nslots, uint32_t *hist) {
     if (nrows == 0) return IGX_OK;
-    if (ndev == 0 || ndev > 64) return igx_fail(ctx, IGX_EINVAL, "hist: ndev must be 1..64");
+    if (ndev > 64) return igx_fail(ctx, IGX_EINVAL, "hist: at most 64 devices");
+    if (ndev && (!dev || !devs)) return igx_fail(ctx, IGX_EINVAL, "hist: device column / list missing");
     if (ncont == 0 || (!cont && ncont != 1)) return igx_fail(ctx, IGX_EINVAL, "hist: bad ncont");
     if (nslots == 0 || nslots > 64 || divisor == 0) return igx_fail(ctx, IGX_EINVAL, "hist: bad nslots/divisor");
+    if (!delta || !hist) return igx_fail(ctx, IGX_EINVAL, "hist: null delta / hist");
     HistArgs a{};
     a.dev = dev;
     a.cont = cont;
     a.delta = delta;
     a.n = nrows;
-    std::vector<std::pair<uint32_t, uint32_t>> dv;
-    for (uint32_t i = 0; i < ndev; ++i) dv.push_back({devs[i], i});
-    std::sort(dv.begin(), dv.end());
-    for (uint32_t i = 1; i < ndev; ++i)
-        if (dv[i].first == dv[i - 1].first) return igx_fail(ctx, IGX_EINVAL, "hist: duplicate device");
-    for (uint32_t i = 0; i < 64; ++i) {
-        a.devs_sorted[i] = i < ndev ? dv[i].first : 0xFFFFFFFFu;
-        a.devs_index[i] = i < ndev ? dv[i].second : 0;
+    for (uint32_t e = 0; e < DEVTAB; ++e) a.dev_key[e] = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < ndev; ++i) {
+        if (devs[i] == 0xFFFFFFFFu) return igx_fail(ctx, IGX_EINVAL, "hist: device 0xffffffff is reserved");
+        uint32_t e = dev_hash(devs[i]);
+        while (a.dev_key[e] != 0xFFFFFFFFu) {
+            if (a.dev_key[e] == devs[i]) return igx_fail(ctx, IGX_EINVAL, "hist: duplicate device");
+            e = (e + 1) & (DEVTAB - 1);
+        }
+        a.dev_key[e] = devs[i];
+        a.dev_idx[e] = (uint8_t)i;
     }
-    a.ndev = ndev;
+    a.single = ndev == 0;
+    a.ndev = ndev ? ndev : 1;
     a.ncont = ncont;
     a.nslots = nslots;
-    const uint64_t nkeys = (uint64_t)ndev * ncont;
-    const uint64_t keys_fit = LDS_BUDGET / (4ull * nslots);
+    const uint64_t nkeys = (uint64_t)a.ndev * ncont;
+    const uint64_t keys_fit = (LDS_BUDGET - 64) / (2ull * nslots);
     a.P = (uint32_t)((nkeys + keys_fit - 1) / keys_fit);
     a.Kp = (uint32_t)((nkeys + a.P - 1) / a.P);
-    const uint32_t part_bytes = a.Kp * nslots * 4;
+    a.rep_words = (a.Kp * nslots + 1) / 2;
+    const uint32_t part_bytes = a.rep_words * 4;
     a.R = std::max<uint32_t>(1, std::min<uint32_t>(TB / 64, LDS_BUDGET / part_bytes));
-    // small histograms: keep several workgroups per CU
-    uint32_t bpc = (part_bytes * a.R <= 32 * 1024) ? 2 : 1;
-    if (a.R > 4 && bpc == 2) a.R = 4;
+    // small histograms: keep two workgroups per CU
+    const uint32_t bpc = (part_bytes * a.R <= 32 * 1024) ? 2 : 1;
+    if (bpc == 2) a.R = std::min<uint32_t>(a.R, 8);
     uint32_t blocks = (uint32_t)ctx->num_cus * bpc;
     blocks = std::max<uint32_t>(8 * a.P, blocks / (8 * a.P) * (8 * a.P));
     a.ngroups = blocks / a.P;
     a.divisor = divisor;
     a.hist = hist;
     const size_t lds = (size_t)part_bytes * a.R;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist<1000>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist<1000000>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist<0>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
-        attr_set = true;
-    }
-    if (divisor == 1000)
-        hipLaunchKernelGGL(k_hist<1000>, dim3(blocks), dim3(TB), lds, ctx->stream, a);
-    else if (divisor == 1000000)
-        hipLaunchKernelGGL(k_hist<1000000>, dim3(blocks), dim3(TB), lds, ctx->stream, a);
-    else
-        hipLaunchKernelGGL(k_hist<0>, dim3(blocks), dim3(TB), lds, ctx->stream, a);
+    const bool vec = (reinterpret_cast<uintptr_t>(dev) | reinterpret_cast<uintptr_t>(cont) |
+                      reinterpret_cast<uintptr_t>(delta)) % 16 == 0 && (dev || a.single);
+    // the vector path loads dev unconditionally: single-key mode without a column scalar-loads
+    const bool use_vec = vec && dev != nullptr;
+    if (divisor == 1000) launch<1000>(a, blocks, lds, ctx->stream, use_vec);
+    else if (divisor == 1000000) launch<1000000>(a, blocks, lds, ctx->stream, use_vec);
+    else if (divisor == 1) launch<1>(a, blocks, lds, ctx->stream, use_vec);
+    else launch<0>(a, blocks, lds, ctx->stream, use_vec);
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }

@@ -260,10 +260,10 @@ def np_mark(typ, pkt, hostip, raddr):
 def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, hist=None):
     torch = torch_mod()
     ctx = context()
-    n = dev.numel()
+    n = delta.numel()
     if hist is None:
-        hist = torch.zeros((len(devs) * ncont, nslots), dtype=torch.uint32, device=dev.device)
-    hd = (C.c_uint32 * len(devs))(*devs)
+        hist = torch.zeros((max(1, len(devs)) * ncont, nslots), dtype=torch.uint32, device=delta.device)
+    hd = (C.c_uint32 * max(1, len(devs)))(*devs)
     ctx.check(ctx.L.igx_hist_log2(ctx.h, ptr(dev), ptr(cont), ptr(delta), n, hd, len(devs),
                                   ncont, divisor, nslots, ptr(hist)))
     return hist

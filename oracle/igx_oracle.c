@@ -394,6 +394,7 @@ typedef struct {
     u64 cond_val;        /* row counts iff cond == cond_val */
     u32 out_width;       /* wrap width in bytes (1,2,4,8) */
     u32 val_signed;      /* SUM over a signed column: values sign-extend (Go int64 math) */
+    u64 div;             /* > 1: add val / div per event (biotop.bpf.c:98,119 `us += delta/1000`) */
 } or_agg;
 
 static inline u64 ld_u(const void *p, u32 w, u64 row) {
@@ -473,6 +474,7 @@ u64 or_groupby(const u8 *keys, u32 kb, u64 n, const u8 *valid, const or_agg *agg
                 const u32 sh = 64 - 8 * A->val_width;
                 add = (u64)(((int64_t)(add << sh)) >> sh);
             }
+            if (A->kind != OR_AGG_COUNT && A->div > 1) add /= A->div;
             u64 *dst = &out_aggs[(u64)a * maxG + g];
             u64 v = *dst + add;
             if (A->out_width < 8) v &= (1ull << (8 * A->out_width)) - 1;
@@ -512,8 +514,10 @@ void or_hist_log2(const u32 *dev, const u32 *cont, const i64 *delta, u64 n, cons
         i64 d = delta[i];
         if (d < 0) continue;
         u32 di = 0;
-        while (di < ndev && devs[di] != dev[i]) di++;
-        if (di == ndev) continue;                    /* unknown device: not counted */
+        if (ndev) {                                  /* ndev == 0: one key (the shipped gadget) */
+            while (di < ndev && devs[di] != dev[i]) di++;
+            if (di == ndev) continue;                /* unknown device: not counted */
+        }
         if (cont && cont[i] >= ncont) continue;      /* unknown container: not counted */
         u64 v = (u64)d / divisor;
         u64 slot = or_log2l(v);

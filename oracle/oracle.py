@@ -418,13 +418,13 @@ def closed_form_perm(key_values, descs, n):
 class _CAgg(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("val_width", C.c_uint32), ("val", C.c_void_p),
                 ("cond_width", C.c_uint32), ("cond", C.c_void_p), ("cond_val", C.c_uint64),
-                ("out_width", C.c_uint32), ("val_signed", C.c_uint32)]
+                ("out_width", C.c_uint32), ("val_signed", C.c_uint32), ("div", C.c_uint64)]
 
 
 def groupby(keys_packed: np.ndarray, aggs, valid=None, base_idx=0, max_groups=None):
     """Generic keyed aggregation in first-occurrence order.  keys_packed: (n, kb) uint8.
     aggs: list of dicts {kind: 'count'|'sum', val: array|None, cond: array|None,
-    cond_val: int, out_width: int}.  Returns (keys (G,kb), aggs (naggs,G) u64, first)."""
+    cond_val: int, out_width: int, div: int (sum of val // div per event)}.  Returns (keys (G,kb), aggs (naggs,G) u64, first)."""
     keys_packed = np.ascontiguousarray(keys_packed, dtype=np.uint8)
     n, kb = keys_packed.shape
     maxG = max_groups or max(1, n)
@@ -444,7 +444,7 @@ def groupby(keys_packed: np.ndarray, aggs, valid=None, base_idx=0, max_groups=No
                          0 if cond is None else cond.dtype.itemsize,
                          0 if cond is None else cond.ctypes.data,
                          int(a.get("cond_val", 0)), int(a.get("out_width", 8)),
-                         int(val is not None and val.dtype.kind == "i")))
+                         int(val is not None and val.dtype.kind == "i"), int(a.get("div", 0))))
     arr = (_CAgg * max(1, len(cag)))(*cag)
     out_keys = np.empty((maxG, kb), dtype=np.uint8)
     out_aggs = np.zeros((max(1, len(aggs)), maxG), dtype=np.uint64)
@@ -463,9 +463,10 @@ def log2l(v: int) -> int:
 
 def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27):
     devs = np.ascontiguousarray(devs, dtype=np.uint32)
-    hist = np.zeros((len(devs) * ncont, nslots), dtype=np.uint32)
-    dev = np.ascontiguousarray(dev, dtype=np.uint32)
-    cont = np.ascontiguousarray(cont, dtype=np.uint32)
+    hist = np.zeros((max(1, len(devs)) * ncont, nslots), dtype=np.uint32)
+    delta = np.ascontiguousarray(delta).view(np.int64)
+    dev = np.ascontiguousarray(np.zeros(len(delta), np.uint32) if dev is None else dev, dtype=np.uint32)
+    cont = np.ascontiguousarray(np.zeros(len(delta), np.uint32) if cont is None else cont, dtype=np.uint32)
     delta = np.ascontiguousarray(delta).view(np.int64)
     lib().or_hist_log2(_p(dev), _p(cont), _p(delta), len(dev), _p(devs), len(devs), ncont,
                        divisor, nslots, _p(hist))
