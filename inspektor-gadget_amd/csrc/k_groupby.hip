@@ -25,13 +25,14 @@
 // in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off table row 1).  No
 // counter is touched per new key.
 //
-// Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 2-way on the key
-// hash, entries hold the full key, its slot and the workgroup's partial aggregates;
+// Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 8-way set associative
+// on the key hash, entries hold the full key, its slot and the workgroup's partial aggregates;
 // first come, never evicted, so the Zipf-hot keys settle in LDS and their events cost only
 // their own input bytes plus LDS atomics.  Misses are queued per wave in LDS and resolved
 // 64 at a time against HBM (a wave pays one probe round trip per 64 misses, not one per
 // iteration in which any lane missed).  The cache is committed with HBM atomics at the end.
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 #include "k_common.h"
@@ -72,15 +73,22 @@ struct GbArgs {
     uint64_t cval[AMAX];
     uint64_t vdiv[AMAX];    // 0: plain value, else value / vdiv (unsigned)
     uint32_t vwidth[AMAX], vsign[AMAX], vcount[AMAX], cwidth[AMAX], hascond[AMAX];
+    // per aggregate: load its value / condition column (1), or reuse aggregate vshare /
+    // cshare's dwords (same column; AMAX = not shared)
+    uint32_t vload[AMAX], cload[AMAX], vshare[AMAX], cshare[AMAX];
+    // load geometry: row stride (0 = nothing to load: dword 0 of the pointer) and the
+    // offset of the high dword (4 for 8-byte columns, else 0)
+    uint32_t vldw[AMAX], cldw[AMAX], vhioff[AMAX], chioff[AMAX], phioff[PMAX], validw;
     uint32_t naggs;
     // scalar predicates (FilterSpec on a <= 8-byte column), AND-ed
     const uint8_t *pptr[PMAX];
     uint64_t pref[PMAX];
     uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
     uint32_t npred;
-    uint32_t lds_entries;   // E (power of two)
+    uint32_t lds_entries;   // E (8 x sets)
     // input
     const uint8_t *valid;   // nullable: rows with 0 are skipped (nil / filtered entries)
+    const uint8_t *validp;  // valid, or the dummy column when there is none (always loaded)
     const uint64_t *fidx;   // nullable: per-row global event index (merging partial groups)
     uint64_t n, base_idx;
     // table
@@ -93,22 +101,29 @@ struct GbArgs {
     uint64_t mask;
     uint32_t max_probe;
     // diagnostics (IGX_GB_DEBUG, never set in production): bit0 stop after load+hash,
-    // bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count hits/misses
+    // bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count hits/misses; in the miss
+    // drain: bit4 no LDS lookup/adopt, bit5 no HBM probe, bit6 no row re-read; bit7 queue
+    // misses and resolve them 64 at a time (the round-1 scheme) instead of at once
     uint32_t dbg;
     unsigned long long *dbg_cnt;
 };
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// Key hash: NH (the UMAC inner hash) over the key's word pairs -- one 32x32->64 multiply
+// per 8 key bytes, sum(( k[2i] + K[2i]) * (k[2i+1] + K[2i+1])) mod 2^64 -- then the murmur3
+// 64-bit finaliser.  Exactness never depends on it (keys are compared in full); it only
+// spreads slots, LDS sets and tags.
+__device__ __forceinline__ uint32_t nh_const(int i) {
+    return 0x9E3779B9u * (uint32_t)(2 * i + 1) + 0x7F4A7C15u;   // odd, distinct per word
+}
 
-// Key hash: one 64-bit multiply per 8 key bytes plus a murmur3 finaliser.  Exactness never
-// depends on it (keys are compared in full); it only spreads slots and LDS sets.
 template <int KW>
 __device__ __forceinline__ uint64_t hash_key(const uint32_t (&k)[KW]) {
     uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)KW;
 #pragma unroll
     for (int w = 0; w < KW; w += 2) {
-        uint64_t x = (uint64_t)k[w] | ((w + 1 < KW) ? ((uint64_t)k[w + 1] << 32) : 0ull);
-        h = rotl64(h ^ (x * 0x9E3779B97F4A7C15ull), 29) + (h << 3);
+        const uint32_t a = k[w] + nh_const(w);
+        const uint32_t b = ((w + 1 < KW) ? k[w + 1] : 0u) + nh_const(w + 1);
+        h += (uint64_t)a * (uint64_t)b;
     }
     h ^= h >> 33;
     h *= 0xFF51AFD7ED558CCDull;
@@ -126,7 +141,7 @@ __device__ __forceinline__ uint32_t ldw(const uint8_t *base, uint64_t off) {
 }
 
 // zero-extended little-endian value of `width` (1, 2, 4 or 8) bytes at row; branch-free
-__device__ __forceinline__ uint64_t ld_val(const uint8_t *base, uint64_t row, uint32_t width) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t ld_val(const uint8_t *base, uint64_t row, uint32_t width) {
     const uint64_t b = row * width;
     const uint32_t lomask = width >= 4 ? 0xFFFFFFFFu : ((1u << (8 * width)) - 1u);
     const uint32_t lo = ldw(base, b) & lomask;
@@ -323,82 +338,143 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
 template <int KW>
 struct LdsCache {
     static constexpr int KP = (KW + 3) & ~3;   // key words padded to 16 B
-    uint32_t *st;      // E: ST_EMPTY, ST_BUSY or the HBM slot
-    uint64_t *tag;     // E
+    uint32_t *tag;     // E: 0 = empty, else the low hash word | 1 (set once, by the claimer)
+    uint32_t *st;      // E: ST_EMPTY until published, then the HBM slot
     uint32_t *key;     // E x KP
     uint64_t *agg;     // naggs x E
     uint64_t *first;   // E
-    uint32_t E;
+    uint32_t E;        // 8 x nsets
+    uint32_t nsets;
 };
 
+// full key compare: every quad is loaded before any is compared (a short-circuit compare
+// becomes one LDS round trip per quad)
 template <int KW>
 __device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, const uint32_t (&k)[KW]) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(c.key + (uint64_t)e * LdsCache<KW>::KP);
-    bool eq = true;
+    constexpr int NQ = LdsCache<KW>::KP / 4;
+    const uint4 *p = reinterpret_cast<const uint4 *>(c.key) + (uint64_t)e * (LdsCache<KW>::KP / 4);
+    uint4 q[NQ];
 #pragma unroll
-    for (int q = 0; q < LdsCache<KW>::KP / 4; ++q) {
-        const uint4 v = p[q];
-        if (4 * q + 0 < KW) eq = eq && v.x == k[4 * q + 0];
-        if (4 * q + 1 < KW) eq = eq && v.y == k[4 * q + 1];
-        if (4 * q + 2 < KW) eq = eq && v.z == k[4 * q + 2];
-        if (4 * q + 3 < KW) eq = eq && v.w == k[4 * q + 3];
+    for (int i = 0; i < NQ; ++i) q[i] = p[i];
+    // the padding words are compared too (lds_adopt zeroes them): the loads stay whole
+    // 16-byte reads instead of being narrowed to the key's words and split
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        diff |= q[i].x ^ (4 * i + 0 < KW ? k[4 * i + 0] : 0u);
+        diff |= q[i].y ^ (4 * i + 1 < KW ? k[4 * i + 1] : 0u);
+        diff |= q[i].z ^ (4 * i + 2 < KW ? k[4 * i + 2] : 0u);
+        diff |= q[i].w ^ (4 * i + 3 < KW ? k[4 * i + 3] : 0u);
     }
-    return eq;
+    return diff == 0;
 }
 
 // ---- per-row pieces ------------------------------------------------------------------
-// Loads every input byte of the row (all in flight together), applies the predicates and
-// produces the aggregate contributions.  Loads guarded only by uniform count checks leave
-// their register undefined on the other arm, so no copy -- and no wait -- is needed at the
-// join.
+// Every input dword of the row is loaded unconditionally first (unused predicate and
+// aggregate slots point at a readable dummy column, set up by the host), and only then
+// combined.  A load whose value is used inside a branch forces the wait into that branch,
+// so each guarded column used to cost a memory round trip of its own; issued together
+// they retire under one wait.
+__device__ __forceinline__ uint32_t ldd(const uint8_t *base, uint64_t off) {
+    return *reinterpret_cast<const uint32_t *>(base + (off & ~3ull));
+}
+
+// zero-extended value of `width` bytes from the aligned dwords lo (holding its first byte)
+// and hi (the next dword; used for width 8 only)
+__device__ __forceinline__ uint64_t assemble(uint32_t lo, uint32_t hi, uint64_t off, uint32_t width) {
+    const uint32_t lomask = width >= 4 ? 0xFFFFFFFFu : ((1u << (8 * width)) - 1u);
+    const uint32_t l = (lo >> ((uint32_t)(off & 3u) * 8u)) & lomask;
+    return (uint64_t)l | ((uint64_t)(width == 8 ? hi : 0u) << 32);
+}
+
 template <class L>
 __device__ __forceinline__ bool load_row(const GbArgs &a, uint64_t row, uint32_t (&k)[L::KW], uint64_t (&v)[AMAX]) {
-    const uint32_t vb = a.valid ? (ldw(a.valid, row) & 0xFFu) : 1u;
-    uint64_t pv[PMAX];
+    // unconditional loads; slots with nothing to load read dword 0 of the dummy column
+    // (width 0: one cached line for the whole wave)
+    const uint32_t vraw = ldd(a.validp, row * a.validw);
+    uint32_t plo[PMAX], phi[PMAX], vlo[AMAX], vhi[AMAX], clo[AMAX], chi[AMAX];
 #pragma unroll
-    for (int p = 0; p < PMAX; ++p)
-        if (p < (int)a.npred) pv[p] = ld_val(a.pptr[p], row, a.pwidth[p]);
+    for (int p = 0; p < PMAX; ++p) {
+        const uint64_t b = row * a.pwidth[p];
+        plo[p] = ldd(a.pptr[p], b);
+        phi[p] = ldd(a.pptr[p], b + a.phioff[p]);
+    }
     L::load(a, row, k);
-    uint64_t cv[AMAX];
 #pragma unroll
     for (int x = 0; x < AMAX; ++x) {
-        if (x < (int)a.naggs) {
-            v[x] = ld_val(a.vptr[x], row, a.vwidth[x]);
-            cv[x] = ld_val(a.cptr[x], row, a.cwidth[x]);
+        const uint64_t bv = row * a.vldw[x], bc = row * a.cldw[x];
+        vlo[x] = ldd(a.vptr[x], bv);
+        vhi[x] = ldd(a.vptr[x], bv + a.vhioff[x]);
+        clo[x] = ldd(a.cptr[x], bc);
+        chi[x] = ldd(a.cptr[x], bc + a.chioff[x]);
+    }
+    // aggregates reading a column an earlier one already loaded reuse its dwords
+#pragma unroll
+    for (int x = 1; x < AMAX; ++x) {
+#pragma unroll
+        for (int y = 0; y < x; ++y) {
+            if (a.vshare[x] == (uint32_t)y) { vlo[x] = vlo[y]; vhi[x] = vhi[y]; }
+            if (a.cshare[x] == (uint32_t)y) { clo[x] = clo[y]; chi[x] = chi[y]; }
         }
     }
-    bool ok = vb != 0;
+    bool ok = !a.valid || ((vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
 #pragma unroll
-    for (int p = 0; p < PMAX; ++p)
-        if (p < (int)a.npred) ok = ok && pred_scalar(pv[p], a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p],
-                                     a.pcnt[p]);
+    for (int p = 0; p < PMAX; ++p) {
+        if (p < (int)a.npred) {
+            const uint64_t pv = assemble(plo[p], phi[p], row * a.pwidth[p], a.pwidth[p]);
+            ok = ok && pred_scalar(pv, a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p], a.pcnt[p]);
+        }
+    }
 #pragma unroll
     for (int x = 0; x < AMAX; ++x) {
+        uint64_t val = 0;
         if (x < (int)a.naggs) {
-            uint64_t val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(v[x], a.vwidth[x]) : v[x]);
+            const uint64_t raw = assemble(vlo[x], vhi[x], row * a.vwidth[x], a.vwidth[x]);
+            const uint64_t cv = assemble(clo[x], chi[x], row * a.cwidth[x], a.cwidth[x]);
+            val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(raw, a.vwidth[x]) : raw);
             if (a.vdiv[x]) val /= a.vdiv[x];
-            if (a.hascond[x] && cv[x] != a.cval[x]) val = 0;
-            v[x] = val;
-        } else {
-            v[x] = 0;
+            if (a.hascond[x] && cv != a.cval[x]) val = 0;
         }
+        v[x] = val;
     }
     return ok;
 }
 
-// LDS probing: linear over LDS_PROBE entries from the hash's home entry.  Entries are never
-// evicted, so an EMPTY entry ends the search (a key being adopted right now may be missed:
-// its event then takes the HBM path, which is only slower).
-constexpr int LDS_PROBE = 8;
+// The LDS cache is 8-way set associative: the key hash's high word picks a set of 8
+// consecutive entries, its low word (| 1) is the entry's tag.  A lookup reads the set's 8
+// tags with two 16-byte LDS loads and compares full keys only on a tag match, so a miss
+// costs two LDS reads, not a walk.  Entries are first come, never evicted: the claimer
+// CASes the tag from 0, writes the key, then publishes the HBM slot in `st` (release); a
+// reader that matches a tag but still sees ST_EMPTY treats it as a miss (its event takes
+// the HBM path, which is only slower).
+__device__ __forceinline__ uint32_t lds_tag(uint64_t h) { return (uint32_t)h | 1u; }
+
+template <int KW>
+__device__ __forceinline__ uint32_t lds_set(const LdsCache<KW> &c, uint64_t h) {
+    return (uint32_t)(((h >> 32) * (uint64_t)c.nsets) >> 32) * 8u;
+}
+
+template <int KW>
+__device__ __forceinline__ void lds_tags(const LdsCache<KW> &c, uint32_t base, uint32_t (&tg)[8]) {
+    const uint4 t0 = *reinterpret_cast<const uint4 *>(c.tag + base);
+    const uint4 t1 = *reinterpret_cast<const uint4 *>(c.tag + base + 4);
+    tg[0] = t0.x; tg[1] = t0.y; tg[2] = t0.z; tg[3] = t0.w;
+    tg[4] = t1.x; tg[5] = t1.y; tg[6] = t1.z; tg[7] = t1.w;
+}
 
 template <int KW>
 __device__ __forceinline__ int lds_lookup(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t &gs) {
-    const uint32_t e0 = (uint32_t)(h >> 40);
-    for (int j = 0; j < LDS_PROBE; ++j) {
-        const uint32_t e = (e0 + (uint32_t)j) & (c.E - 1);
+    const uint32_t base = lds_set(c, h), t = lds_tag(h);
+    uint32_t tg[8];
+    lds_tags(c, base, tg);
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m |= (tg[j] == t ? 1u : 0u) << j;
+    while (m) {   // usually zero or one candidate
+        const uint32_t e = base + (uint32_t)(__builtin_ffs((int)m) - 1);
+        m &= m - 1;
         const uint32_t s = __hip_atomic_load(&c.st[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (s == ST_EMPTY) break;
-        if (s < ST_BUSY && c.tag[e] == h && lds_key_eq<KW>(c, e, k)) {
+        if (s < ST_BUSY && lds_key_eq<KW>(c, e, k)) {
             gs = s;
             return (int)e;
         }
@@ -406,25 +482,25 @@ __device__ __forceinline__ int lds_lookup(const LdsCache<KW> &c, const uint32_t 
     return -1;
 }
 
-// adopt an empty LDS entry for a key just resolved in HBM (first come, never evicted)
+// adopt a free entry of the key's set for a key just resolved in HBM
 template <int KW>
 __device__ __forceinline__ int lds_adopt(const LdsCache<KW> &c, const uint32_t (&k)[KW], uint64_t h, uint32_t gs) {
-    const uint32_t e0 = (uint32_t)(h >> 40);
-    for (int j = 0; j < LDS_PROBE; ++j) {
-        const uint32_t e = (e0 + (uint32_t)j) & (c.E - 1);
-        if (c.st[e] == ST_EMPTY) {
-            if (atomicCAS(&c.st[e], ST_EMPTY, ST_BUSY) == ST_EMPTY) {
-                c.tag[e] = h;
-                uint32_t *kp = c.key + (uint64_t)e * LdsCache<KW>::KP;
+    const uint32_t base = lds_set(c, h);
+    uint32_t tg[8];
+    lds_tags(c, base, tg);
+    uint32_t m = 0;
 #pragma unroll
-                for (int w = 0; w < KW; ++w) kp[w] = k[w];
-                __hip_atomic_store(&c.st[e], gs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return (int)e;
-            }
-            return -1;   // one attempt only: a lost race falls back to HBM atomics
-        }
-    }
-    return -1;
+    for (int j = 0; j < 8; ++j) m |= (tg[j] == 0 ? 1u : 0u) << j;
+    if (!m) return -1;   // set full
+    const uint32_t e = base + (uint32_t)(__builtin_ffs((int)m) - 1);
+    if (atomicCAS(&c.tag[e], 0u, lds_tag(h)) != 0u) return -1;   // lost the race: HBM path
+    uint4 *kp = reinterpret_cast<uint4 *>(c.key) + (uint64_t)e * (LdsCache<KW>::KP / 4);
+#pragma unroll
+    for (int i = 0; i < LdsCache<KW>::KP / 4; ++i)
+        kp[i] = make_uint4(4 * i + 0 < KW ? k[4 * i + 0] : 0u, 4 * i + 1 < KW ? k[4 * i + 1] : 0u,
+                           4 * i + 2 < KW ? k[4 * i + 2] : 0u, 4 * i + 3 < KW ? k[4 * i + 3] : 0u);
+    __hip_atomic_store(&c.st[e], gs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (int)e;
 }
 
 __device__ __forceinline__ uint64_t row_gidx(const GbArgs &a, uint64_t row) {
@@ -438,7 +514,7 @@ __device__ __forceinline__ unsigned long long *rec_agg(const GbArgs &a, uint32_t
     return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words + 1 + x);
 }
 
-template <int KW>
+template <int KW, bool DBG>
 __device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &c, int slot, uint32_t gs,
                                            const uint64_t (&v)[AMAX], uint64_t gidx, uint64_t first_ins) {
     if (slot >= 0) {
@@ -447,7 +523,7 @@ __device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &
             if (x < (int)a.naggs && v[x])
                 atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
         atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
-    } else if (!(a.dbg & 4u)) {
+    } else if (!(DBG && (a.dbg & 4u))) {
 #pragma unroll
         for (int x = 0; x < AMAX; ++x)
             if (x < (int)a.naggs && v[x]) atomicAdd(rec_agg(a, gs, x), (unsigned long long)v[x]);
@@ -456,7 +532,7 @@ __device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &
 }
 
 // resolve `cnt` queued misses of this wave against the HBM table, one per lane
-template <class L>
+template <class L, bool DBG>
 __device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::KW> &c, const uint32_t *q,
                                              uint32_t qhead, uint32_t cnt, uint32_t lane) {
     constexpr int KW = L::KW;
@@ -465,43 +541,57 @@ __device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::
         const uint64_t row = q[(qhead + lane) % QCAP];
         uint32_t k[KW];
         uint64_t v[AMAX];
-        (void)load_row<L>(a, row, k, v);      // predicates already passed
+        if (DBG && (a.dbg & 64u)) {   // diagnostics: no re-read (synthetic key)
+#pragma unroll
+            for (int w = 0; w < KW; ++w) k[w] = (uint32_t)row * (uint32_t)(w + 1);
+#pragma unroll
+            for (int x = 0; x < AMAX; ++x) v[x] = 1;
+        } else {
+            (void)load_row<L>(a, row, k, v);      // predicates already passed
+        }
         const uint64_t h = hash_key<KW>(k);
         uint32_t gs = SLOT_OVF;
         uint64_t first_ins = 0;
         const uint64_t gidx = row_gidx(a, row);
-        int slot = lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
+        int slot = (DBG && (a.dbg & 16u)) ? -1 : lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
         if (slot < 0) {
-            gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
-            if (gs != SLOT_OVF) slot = lds_adopt<KW>(c, k, h, gs);
+            if (DBG && (a.dbg & 32u)) {   // diagnostics: no probe
+                gs = (uint32_t)((h >> 17) & a.mask);
+                first_ins = 0;
+            } else {
+                gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
+            }
+            if (gs != SLOT_OVF && !(DBG && (a.dbg & 16u))) slot = lds_adopt<KW>(c, k, h, gs);
         }
-        if (gs != SLOT_OVF) accumulate<KW>(a, c, slot, gs, v, gidx, first_ins);
+        if (gs != SLOT_OVF) accumulate<KW, DBG>(a, c, slot, gs, v, gidx, first_ins);
     }
     __builtin_amdgcn_wave_barrier();
 }
 
-template <class L>
+template <class L, bool DBG>
 __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     constexpr int KW = L::KW;
     extern __shared__ uint64_t lds[];
     LdsCache<KW> c;
     c.E = a.lds_entries;
+    c.nsets = a.lds_entries / 8;
     const uint32_t E = c.E;
-    c.tag = lds;
-    c.first = lds + E;
-    c.agg = lds + 2 * E;
-    c.key = reinterpret_cast<uint32_t *>(lds + (2 + a.naggs) * E);
+    c.first = lds;
+    c.agg = lds + E;
+    c.key = reinterpret_cast<uint32_t *>(lds + (1 + a.naggs) * E);
     c.st = c.key + (uint64_t)E * LdsCache<KW>::KP;
+    c.tag = c.st + E;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t *q = c.st + E + wave * QCAP;
+    uint32_t *q = c.tag + E + wave * QCAP;
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         c.st[e] = ST_EMPTY;
+        c.tag[e] = 0;
         c.first[e] = ~0ull;
         for (uint32_t x = 0; x < a.naggs; ++x) c.agg[x * E + e] = 0;
     }
     __syncthreads();
 
-    uint32_t qhead = 0, qn = 0;   // wave-uniform
+    uint32_t qhead = 0, qn = 0;   // wave-uniform (DBG bit 7: queued miss path)
     const uint64_t stride = (uint64_t)gridDim.x * GTB;
     for (uint64_t base = (uint64_t)blockIdx.x * GTB + wave * 64; base < a.n; base += stride) {
         const uint64_t row = base + lane;
@@ -511,30 +601,52 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
             uint64_t v[AMAX];
             const bool ok = load_row<L>(a, row, k, v);
             const uint64_t h = hash_key<KW>(k);
-            if (a.dbg & 1u) {
+            if (DBG && (a.dbg & 1u)) {
                 if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live
             } else if (ok) {
                 uint32_t gs = SLOT_OVF;
                 const int slot = lds_lookup<KW>(c, k, h, gs);
-                if (a.dbg & 8u) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
-                if (slot >= 0) accumulate<KW>(a, c, slot, gs, v, row_gidx(a, row), 0);
-                else miss = !(a.dbg & 2u);
+                if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
+                if (slot >= 0) {
+                    if (!(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
+                        accumulate<KW, DBG>(a, c, slot, gs, v, row_gidx(a, row), 0);
+                } else if (DBG && (a.dbg & 128u)) {
+                    miss = !(a.dbg & 2u);
+                } else if (!(DBG && (a.dbg & 2u))) {
+                    // resolve the miss now, while the row is in registers: HBM probe, adopt a
+                    // free LDS entry if the set has one, accumulate
+                    const uint64_t gidx = row_gidx(a, row);
+                    uint64_t first_ins = 0;
+                    if (DBG && (a.dbg & 256u)) {   // diagnostics: no probe (a hash-derived slot)
+                        gs = (uint32_t)((h >> 17) & a.mask);
+                    } else {
+                        gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
+                    }
+                    if (gs != SLOT_OVF) {
+                        const int ad = lds_adopt<KW>(c, k, h, gs);
+                        accumulate<KW, DBG>(a, c, ad, gs, v, gidx, first_ins);
+                    }
+                }
             }
         }
-        const uint64_t m = __ballot(miss);
-        if (miss) q[(qhead + qn + __popcll(m & lanemask_lt())) % QCAP] = (uint32_t)row;
-        qn += (uint32_t)__popcll(m);
-        if (qn >= 64) {
-            drain_misses<L>(a, c, q, qhead, 64, lane);
-            qhead = (qhead + 64) % QCAP;
-            qn -= 64;
+        if constexpr (DBG) {
+            const uint64_t m = __ballot(miss);
+            if (miss) q[(qhead + qn + __popcll(m & lanemask_lt())) % QCAP] = (uint32_t)row;
+            qn += (uint32_t)__popcll(m);
+            if (qn >= 64) {
+                drain_misses<L, DBG>(a, c, q, qhead, 64, lane);
+                qhead = (qhead + 64) % QCAP;
+                qn -= 64;
+            }
         }
     }
-    while (qn) {
-        const uint32_t cnt = qn < 64 ? qn : 64;
-        drain_misses<L>(a, c, q, qhead, cnt, lane);
-        qhead = (qhead + cnt) % QCAP;
-        qn -= cnt;
+    if constexpr (DBG) {
+        while (qn) {
+            const uint32_t cnt = qn < 64 ? qn : 64;
+            drain_misses<L, DBG>(a, c, q, qhead, cnt, lane);
+            qhead = (qhead + cnt) % QCAP;
+            qn -= cnt;
+        }
     }
 
     __syncthreads();
@@ -830,21 +942,35 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     return IGX_OK;
 }
 
-constexpr size_t GB_LDS_BUDGET = 120 * 1024;   // cache; + 8 KB of miss queues
+constexpr size_t GB_LDS_BUDGET = 148 * 1024;   // cache; + 8 KB of miss queues
 
-template <class L>
-static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+template <class L, bool DBG>
+static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BUDGET + 8192);
         attr = true;
     }
-    const size_t entry = 4 + 8 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
-    uint32_t E = 8192;
-    while (E > 64 && E * entry > GB_LDS_BUDGET) E >>= 1;
+    const size_t entry = 4 + 4 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
+    const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, GB_LDS_BUDGET / (8 * entry)));
+    const uint32_t E = 8 * nsets;
     a.lds_entries = E;
-    hipLaunchKernelGGL(k_groupby<L>, dim3(blocks), dim3(GTB), E * entry + (GTB / 64) * QCAP * 4, ctx->stream, a);
+    hipLaunchKernelGGL((k_groupby<L, DBG>), dim3(blocks), dim3(GTB), E * entry + (GTB / 64) * QCAP * 4,
+                       ctx->stream, a);
+}
+
+// The diagnostic variants (IGX_GB_DEBUG) are compiled for the top-tcp key only, so the
+// production kernels carry none of their code.
+template <class L>
+static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+    if constexpr (std::is_same<L, StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>>::value) {
+        if (a.dbg) {
+            launch_gb_as<L, true>(ctx, a, blocks);
+            return;
+        }
+    }
+    launch_gb_as<L, false>(ctx, a, blocks);
 }
 
 extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
@@ -891,6 +1017,10 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         a.kmask[w] = 0;
     }
     a.naggs = t->naggs;
+    for (uint32_t x = t->naggs; x < AMAX; ++x) {   // unused slots are still loaded (load_row)
+        a.vptr[x] = a.cptr[x] = dummy;
+        a.vwidth[x] = a.cwidth[x] = 1;
+    }
     for (uint32_t x = 0; x < t->naggs; ++x) {
         const igx_agg &g = t->aggs[x];
         a.vcount[x] = g.kind == IGX_AGG_COUNT;
@@ -924,6 +1054,27 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
             a.hascond[x] = 1;
         }
     }
+    for (uint32_t x = 0; x < AMAX; ++x) {
+        a.vshare[x] = a.cshare[x] = AMAX;
+        a.vload[x] = x < t->naggs && !a.vcount[x];
+        a.cload[x] = x < t->naggs && a.hascond[x];
+        for (uint32_t y = 0; y < x; ++y) {
+            if (a.vload[x] && a.vshare[x] == AMAX && a.vload[y] && a.vptr[y] == a.vptr[x] && a.vwidth[y] == a.vwidth[x]) {
+                a.vshare[x] = y;
+                a.vload[x] = 0;
+            }
+            if (a.cload[x] && a.cshare[x] == AMAX && a.cload[y] && a.cptr[y] == a.cptr[x] && a.cwidth[y] == a.cwidth[x]) {
+                a.cshare[x] = y;
+                a.cload[x] = 0;
+            }
+        }
+    }
+    for (uint32_t x = 0; x < AMAX; ++x) {
+        a.vldw[x] = a.vload[x] ? a.vwidth[x] : 0;
+        a.cldw[x] = a.cload[x] ? a.cwidth[x] : 0;
+        a.vhioff[x] = a.vload[x] && a.vwidth[x] == 8 ? 4 : 0;
+        a.chioff[x] = a.cload[x] && a.cwidth[x] == 8 ? 4 : 0;
+    }
     if (npreds > PMAX) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: more than %d predicates", PMAX);
     for (uint32_t p = 0; p < npreds; ++p) {
         const igx_pred &q = preds[p];
@@ -952,8 +1103,15 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         for (uint32_t b = 0; b < nb; ++b) r |= (uint64_t)q.ref[b] << (8 * b);
         a.pref[p] = r;
     }
+    for (uint32_t p = npreds; p < PMAX; ++p) {
+        a.pptr[p] = dummy;
+        a.pwidth[p] = 0;
+    }
+    for (uint32_t p = 0; p < PMAX; ++p) a.phioff[p] = a.pwidth[p] == 8 ? 4 : 0;
     a.npred = npreds;
     a.valid = valid;
+    a.validp = valid ? valid : dummy;
+    a.validw = valid ? 1 : 0;
     a.fidx = nullptr;
     if (idx_col != IGX_NO_COL) {
         if (idx_col >= ncols || cols[idx_col].width != 8)
