@@ -28,9 +28,11 @@
 // Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 8-way set associative
 // on the key hash, entries hold the full key, its slot and the workgroup's partial aggregates;
 // first come, never evicted, so the Zipf-hot keys settle in LDS and their events cost only
-// their own input bytes plus LDS atomics.  Misses are queued per wave in LDS and resolved
-// 64 at a time against HBM (a wave pays one probe round trip per 64 misses, not one per
-// iteration in which any lane missed).  The cache is committed with HBM atomics at the end.
+// their own input bytes plus LDS atomics.  A miss is resolved at once, while its row is in
+// registers: HBM probe, adoption of a free LDS entry when its set has one, and otherwise
+// its HBM updates go to the server wave through an LDS ring (see "HBM atomics through an
+// LDS ring").  Fifteen waves stream rows, the sixteenth issues the ring's atomics.  The
+// cache is committed with HBM atomics at the end.
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -46,7 +48,6 @@ constexpr int PMAX = 2;   // more predicates: run igx_filter first
 constexpr int GTB = 1024;
 constexpr uint32_t ST_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t ST_BUSY = 0xFFFFFFFEu;
-constexpr uint32_t QCAP = 128;   // per-wave miss queue (row ids) in LDS
 
 __host__ __device__ constexpr uint32_t koff_of(int kw) { return (uint32_t)((4 * kw + 7) & ~7); }
 __host__ __device__ constexpr uint32_t pow2_at_least(uint32_t b) {
@@ -100,10 +101,9 @@ struct GbArgs {
     uint32_t *err;
     uint64_t mask;
     uint32_t max_probe;
-    // diagnostics (IGX_GB_DEBUG, never set in production): bit0 stop after load+hash,
-    // bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count hits/misses; in the miss
-    // drain: bit4 no LDS lookup/adopt, bit5 no HBM probe, bit6 no row re-read; bit7 queue
-    // misses and resolve them 64 at a time (the round-1 scheme) instead of at once
+    // diagnostics (IGX_GB_DEBUG; compiled into the top-tcp key's debug kernel only):
+    // bit0 stop after load+hash, bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count
+    // hits/misses, bit8 no HBM probe (a hash-derived slot), bit9 no LDS accumulate on hits
     uint32_t dbg;
     unsigned long long *dbg_cnt;
 };
@@ -267,17 +267,27 @@ __device__ __forceinline__ void load_rec(__amdgpu_buffer_rsrc_t rs, uint32_t off
 // slot's first_ins (claiming event index).  An event with a larger index never needs the
 // atomicMin on the value record's first: the group's first is min(first_ins, that field).
 template <int KW>
+constexpr int probe_quads() { return (int)((koff_of(KW) + 16 + 15) / 16); }   // key, tag, ready
+
+// the home slot's record, issued early so its round trip overlaps other work
+template <int KW>
+__device__ __forceinline__ void probe_issue(const GbArgs &a, uint64_t h, uint32_t (&d)[probe_quads<KW>() * 4]) {
+    load_rec<probe_quads<KW>()>(rec_rsrc(a), (uint32_t)(((h >> 17) & a.mask) * a.krec_len), d);
+}
+
+// d holds the home slot's record (probe_issue)
+template <int KW>
 __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
-                                                   uint64_t gidx, uint64_t &first_ins) {
+                                                   uint64_t gidx, uint64_t &first_ins,
+                                                   uint32_t (&d)[probe_quads<KW>() * 4]) {
     constexpr uint32_t KOFF = koff_of(KW);
-    constexpr int NQ = (int)((KOFF + 16 + 15) / 16);   // covers key, tag, ready
+    constexpr int NQ = probe_quads<KW>();
     const uint64_t tag = h | 1ull;
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     uint64_t s = (h >> 17) & a.mask;
     for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
         const uint32_t off = (uint32_t)(s * a.krec_len);
-        uint32_t d[NQ * 4];
-        load_rec<NQ>(rs, off, d);
+        if (probe) load_rec<NQ>(rs, off, d);
         uint8_t *r = a.krec + off;
         uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
         uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
@@ -387,46 +397,66 @@ __device__ __forceinline__ uint64_t assemble(uint32_t lo, uint32_t hi, uint64_t 
     return (uint64_t)l | ((uint64_t)(width == 8 ? hi : 0u) << 32);
 }
 
-template <class L>
-__device__ __forceinline__ bool load_row(const GbArgs &a, uint64_t row, uint32_t (&k)[L::KW], uint64_t (&v)[AMAX]) {
+// The raw dwords of one row: issued by issue_row, combined by decode_row.  The main loop
+// issues row i+1 before it waits for row i's HBM probe, so the two round trips overlap.
+// NA is the number of aggregate slots the kernel carries (2 or 4).
+template <class L, int NA>
+struct RowRaw {
+    uint32_t k[L::KW];
+    uint32_t vraw, plo[PMAX], phi[PMAX], vlo[NA], vhi[NA], clo[NA], chi[NA];
+};
+
+template <class L, int NA>
+__device__ __forceinline__ void issue_row(const GbArgs &a, uint64_t row, RowRaw<L, NA> &R) {
     // unconditional loads; slots with nothing to load read dword 0 of the dummy column
     // (width 0: one cached line for the whole wave)
-    const uint32_t vraw = ldd(a.validp, row * a.validw);
-    uint32_t plo[PMAX], phi[PMAX], vlo[AMAX], vhi[AMAX], clo[AMAX], chi[AMAX];
+    R.vraw = ldd(a.validp, row * a.validw);
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
         const uint64_t b = row * a.pwidth[p];
-        plo[p] = ldd(a.pptr[p], b);
-        phi[p] = ldd(a.pptr[p], b + a.phioff[p]);
+        R.plo[p] = ldd(a.pptr[p], b);
+        R.phi[p] = ldd(a.pptr[p], b + a.phioff[p]);
     }
-    L::load(a, row, k);
+    L::load(a, row, R.k);
 #pragma unroll
-    for (int x = 0; x < AMAX; ++x) {
+    for (int x = 0; x < NA; ++x) {
         const uint64_t bv = row * a.vldw[x], bc = row * a.cldw[x];
-        vlo[x] = ldd(a.vptr[x], bv);
-        vhi[x] = ldd(a.vptr[x], bv + a.vhioff[x]);
-        clo[x] = ldd(a.cptr[x], bc);
-        chi[x] = ldd(a.cptr[x], bc + a.chioff[x]);
+        R.vlo[x] = ldd(a.vptr[x], bv);
+        R.vhi[x] = ldd(a.vptr[x], bv + a.vhioff[x]);
+        R.clo[x] = ldd(a.cptr[x], bc);
+        R.chi[x] = ldd(a.cptr[x], bc + a.chioff[x]);
+    }
+}
+
+template <class L, int NA>
+__device__ __forceinline__ bool decode_row(const GbArgs &a, uint64_t row, const RowRaw<L, NA> &R,
+                                           uint32_t (&k)[L::KW], uint64_t (&v)[NA]) {
+#pragma unroll
+    for (int w = 0; w < L::KW; ++w) k[w] = R.k[w];
+    uint32_t vlo[NA], vhi[NA], clo[NA], chi[NA];
+#pragma unroll
+    for (int x = 0; x < NA; ++x) {
+        vlo[x] = R.vlo[x]; vhi[x] = R.vhi[x]; clo[x] = R.clo[x]; chi[x] = R.chi[x];
     }
     // aggregates reading a column an earlier one already loaded reuse its dwords
 #pragma unroll
-    for (int x = 1; x < AMAX; ++x) {
+    for (int x = 1; x < NA; ++x) {
 #pragma unroll
         for (int y = 0; y < x; ++y) {
             if (a.vshare[x] == (uint32_t)y) { vlo[x] = vlo[y]; vhi[x] = vhi[y]; }
             if (a.cshare[x] == (uint32_t)y) { clo[x] = clo[y]; chi[x] = chi[y]; }
         }
     }
-    bool ok = !a.valid || ((vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
+    bool ok = !a.valid || ((R.vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
         if (p < (int)a.npred) {
-            const uint64_t pv = assemble(plo[p], phi[p], row * a.pwidth[p], a.pwidth[p]);
+            const uint64_t pv = assemble(R.plo[p], R.phi[p], row * a.pwidth[p], a.pwidth[p]);
             ok = ok && pred_scalar(pv, a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p], a.pcnt[p]);
         }
     }
 #pragma unroll
-    for (int x = 0; x < AMAX; ++x) {
+    for (int x = 0; x < NA; ++x) {
         uint64_t val = 0;
         if (x < (int)a.naggs) {
             const uint64_t raw = assemble(vlo[x], vhi[x], row * a.vwidth[x], a.vwidth[x]);
@@ -507,71 +537,135 @@ __device__ __forceinline__ uint64_t row_gidx(const GbArgs &a, uint64_t row) {
     return a.fidx ? a.fidx[row] : a.base_idx + row;
 }
 
+// value-record words as global (address space 1) pointers, so their atomics are global_*
+// instructions: a flat atomic also counts in lgkmcnt and stalls the next LDS wait
 __device__ __forceinline__ unsigned long long *rec_first(const GbArgs &a, uint32_t gs) {
     return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words);
 }
 __device__ __forceinline__ unsigned long long *rec_agg(const GbArgs &a, uint32_t gs, int x) {
     return reinterpret_cast<unsigned long long *>(a.vrec + (uint64_t)gs * a.vrec_words + 1 + x);
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void gadd(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_fetch_add((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gmin(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_fetch_min((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#else
+__device__ inline void gadd(unsigned long long *, unsigned long long) {}   // host pass: never called
+__device__ inline void gmin(unsigned long long *, unsigned long long) {}
+#endif
 
-template <int KW, bool DBG>
-__device__ __forceinline__ void accumulate(const GbArgs &a, const LdsCache<KW> &c, int slot, uint32_t gs,
-                                           const uint64_t (&v)[AMAX], uint64_t gidx, uint64_t first_ins) {
-    if (slot >= 0) {
+template <int KW, int NA>
+__device__ __forceinline__ void lds_accumulate(const GbArgs &a, const LdsCache<KW> &c, int slot,
+                                               const uint64_t (&v)[NA], uint64_t gidx) {
 #pragma unroll
-        for (int x = 0; x < AMAX; ++x)
-            if (x < (int)a.naggs && v[x])
-                atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
-        atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
-    } else if (!(DBG && (a.dbg & 4u))) {
+    for (int x = 0; x < NA; ++x)
+        if (x < (int)a.naggs && v[x])
+            atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
+    atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
+}
+
+// ---- HBM atomics through an LDS ring ---------------------------------------------------
+// A wave's vmcnt counts its stores and atomics with its loads, in issue order, so a miss's
+// memory-side atomics delayed that wave's next load wait by their whole acknowledgement
+// latency (longer than a load's).  Producer waves therefore push each HBM update as a
+// 16-byte ring entry {slot, lap|what, value} into LDS, and one server wave per workgroup
+// issues them; it loads nothing, so nothing ever waits on their acknowledgement.
+constexpr uint32_t ARING = 1024;            // ring entries (16 B each)
+constexpr uint32_t NPROD = GTB / 64 - 1;    // producer waves; the last wave serves the ring
+constexpr uint32_t WHAT_MIN = 15;           // entry kind: atomicMin on `first`
+
+struct Ring {
+    uint2 *lo;            // {slot, (lap << 4) | what}
+    uint64_t *hi;         // value
+    uint32_t *ctl;        // [0] tail (reserved), [1] head (consumed), [2] producers done
+};
+
+__device__ __forceinline__ uint32_t ring_lap(uint32_t p) { return (p / ARING + 1u) << 4; }
+
+// Push this lane's HBM updates (the aggregates it adds, and a first-index minimum when
+// gidx < first_ins) for slot gs.  Called by the active (missing) lanes of a producer wave.
+template <int NA>
+__device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32_t gs, const uint64_t (&v)[NA],
+                                          uint64_t gidx, uint64_t first_ins) {
+    bool has[NA + 1];
+    uint64_t mask[NA + 1];
+    uint32_t total = 0;
 #pragma unroll
-        for (int x = 0; x < AMAX; ++x)
-            if (x < (int)a.naggs && v[x]) atomicAdd(rec_agg(a, gs, x), (unsigned long long)v[x]);
-        if (gidx < first_ins) atomicMin(rec_first(a, gs), (unsigned long long)gidx);
+    for (int x = 0; x <= NA; ++x) {
+        has[x] = x < NA ? (x < (int)a.naggs && v[x] != 0) : gidx < first_ins;
+        mask[x] = __ballot(has[x]);
+        total += (uint32_t)__popcll(mask[x]);
+    }
+    if (!total) return;
+    const uint64_t active = __ballot(true);
+    const uint32_t leader = (uint32_t)__ffsll((long long)active) - 1;
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == leader) base = atomicAdd(&r.ctl[0], total);
+    base = __shfl(base, (int)leader);
+    // wait for room: the server frees entries as it issues them
+    while (base + total - __hip_atomic_load(&r.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > ARING)
+        __builtin_amdgcn_s_sleep(1);
+    uint32_t off = base;
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int x = 0; x <= NA; ++x) {
+        if (has[x]) {
+            const uint32_t p = off + (uint32_t)__popcll(mask[x] & lt);
+            r.hi[p % ARING] = x < NA ? v[x] : gidx;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            r.lo[p % ARING] = make_uint2(gs, ring_lap(p) | (x < NA ? (uint32_t)x : WHAT_MIN));
+        }
+        off += (uint32_t)__popcll(mask[x]);
     }
 }
 
-// resolve `cnt` queued misses of this wave against the HBM table, one per lane
-template <class L, bool DBG>
-__device__ __forceinline__ void drain_misses(const GbArgs &a, const LdsCache<L::KW> &c, const uint32_t *q,
-                                             uint32_t qhead, uint32_t cnt, uint32_t lane) {
-    constexpr int KW = L::KW;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < cnt) {
-        const uint64_t row = q[(qhead + lane) % QCAP];
-        uint32_t k[KW];
-        uint64_t v[AMAX];
-        if (DBG && (a.dbg & 64u)) {   // diagnostics: no re-read (synthetic key)
-#pragma unroll
-            for (int w = 0; w < KW; ++w) k[w] = (uint32_t)row * (uint32_t)(w + 1);
-#pragma unroll
-            for (int x = 0; x < AMAX; ++x) v[x] = 1;
-        } else {
-            (void)load_row<L>(a, row, k, v);      // predicates already passed
+// the server wave: issue ring entries in order until every producer is done and the ring
+// is empty
+template <bool DBG>
+__device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint32_t lane) {
+    uint32_t head = 0;
+    for (;;) {
+        const uint32_t t = __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (t == head) {
+            if (__hip_atomic_load(&r.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == NPROD &&
+                __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == head)
+                break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
         }
-        const uint64_t h = hash_key<KW>(k);
-        uint32_t gs = SLOT_OVF;
-        uint64_t first_ins = 0;
-        const uint64_t gidx = row_gidx(a, row);
-        int slot = (DBG && (a.dbg & 16u)) ? -1 : lds_lookup<KW>(c, k, h, gs);   // another lane may have adopted it since
-        if (slot < 0) {
-            if (DBG && (a.dbg & 32u)) {   // diagnostics: no probe
-                gs = (uint32_t)((h >> 17) & a.mask);
-                first_ins = 0;
-            } else {
-                gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
+        const uint32_t n = min(t - head, 64u);
+        if (lane < n) {
+            const uint32_t p = head + lane;
+            uint64_t w;
+            while (((uint32_t)((w = __hip_atomic_load(reinterpret_cast<uint64_t *>(&r.lo[p % ARING]),
+                                                      __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) &
+                    ~15u) != ring_lap(p))
+                __builtin_amdgcn_s_sleep(1);
+            const uint64_t val = r.hi[p % ARING];
+            const uint32_t slot = (uint32_t)w, what = (uint32_t)(w >> 32) & 15u;
+            if (!(DBG && (a.dbg & 4u))) {
+                if (what == WHAT_MIN) gmin(rec_first(a, slot), val);
+                else gadd(rec_agg(a, slot, (int)what), val);
             }
-            if (gs != SLOT_OVF && !(DBG && (a.dbg & 16u))) slot = lds_adopt<KW>(c, k, h, gs);
         }
-        if (gs != SLOT_OVF) accumulate<KW, DBG>(a, c, slot, gs, v, gidx, first_ins);
+        head += n;
+        if (lane == 0) __hip_atomic_store(&r.ctl[1], head, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __builtin_amdgcn_wave_barrier();
 }
 
-template <class L, bool DBG>
+template <class L, bool DBG, int NA>
 __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     constexpr int KW = L::KW;
+    // PIPE: issue the next row's loads before waiting for this row's probe.  It overlaps
+    // the two round trips but needs a second row of registers: measured slower for the
+    // 18-word top-tcp key (128 VGPRs + scratch spills), so it is off.
+    constexpr bool PIPE = false;
     extern __shared__ uint64_t lds[];
+    __shared__ uint32_t ring_ctl[4];
     LdsCache<KW> c;
     c.E = a.lds_entries;
     c.nsets = a.lds_entries / 8;
@@ -581,72 +675,68 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     c.key = reinterpret_cast<uint32_t *>(lds + (1 + a.naggs) * E);
     c.st = c.key + (uint64_t)E * LdsCache<KW>::KP;
     c.tag = c.st + E;
+    Ring r;
+    r.hi = reinterpret_cast<uint64_t *>(c.tag + E);   // E is a multiple of 8: 8-B aligned
+    r.lo = reinterpret_cast<uint2 *>(r.hi + ARING);
+    r.ctl = ring_ctl;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t *q = c.tag + E + wave * QCAP;
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         c.st[e] = ST_EMPTY;
         c.tag[e] = 0;
         c.first[e] = ~0ull;
         for (uint32_t x = 0; x < a.naggs; ++x) c.agg[x * E + e] = 0;
     }
+    for (uint32_t e = threadIdx.x; e < ARING; e += GTB) r.lo[e] = make_uint2(0, 0);
+    if (threadIdx.x < 4) ring_ctl[threadIdx.x] = 0;
     __syncthreads();
 
-    uint32_t qhead = 0, qn = 0;   // wave-uniform (DBG bit 7: queued miss path)
-    const uint64_t stride = (uint64_t)gridDim.x * GTB;
-    for (uint64_t base = (uint64_t)blockIdx.x * GTB + wave * 64; base < a.n; base += stride) {
-        const uint64_t row = base + lane;
-        bool miss = false;
-        if (row < a.n) {
+    if (wave == NPROD) {
+        ring_serve<DBG>(a, r, lane);
+    } else {
+        constexpr uint32_t PTB = NPROD * 64;   // rows per workgroup step
+        const uint64_t stride = (uint64_t)gridDim.x * PTB;
+        uint64_t base = (uint64_t)blockIdx.x * PTB + wave * 64;
+        RowRaw<L, NA> R;
+        if (base < a.n) issue_row<L, NA>(a, min(base + lane, a.n - 1), R);
+        for (; base < a.n; base += stride) {
+            const uint64_t row = base + lane;
             uint32_t k[KW];
-            uint64_t v[AMAX];
-            const bool ok = load_row<L>(a, row, k, v);
+            uint64_t v[NA];
+            bool ok = decode_row<L, NA>(a, row, R, k, v) && row < a.n;
             const uint64_t h = hash_key<KW>(k);
-            if (DBG && (a.dbg & 1u)) {
+            if (DBG && (a.dbg & 1u)) {   // diagnostics: load + hash only
                 if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live
-            } else if (ok) {
-                uint32_t gs = SLOT_OVF;
-                const int slot = lds_lookup<KW>(c, k, h, gs);
+                ok = false;
+            }
+            uint32_t gs = SLOT_OVF;
+            int slot = -1;
+            if (ok) {
+                slot = lds_lookup<KW>(c, k, h, gs);
                 if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
-                if (slot >= 0) {
-                    if (!(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
-                        accumulate<KW, DBG>(a, c, slot, gs, v, row_gidx(a, row), 0);
-                } else if (DBG && (a.dbg & 128u)) {
-                    miss = !(a.dbg & 2u);
-                } else if (!(DBG && (a.dbg & 2u))) {
-                    // resolve the miss now, while the row is in registers: HBM probe, adopt a
-                    // free LDS entry if the set has one, accumulate
-                    const uint64_t gidx = row_gidx(a, row);
-                    uint64_t first_ins = 0;
-                    if (DBG && (a.dbg & 256u)) {   // diagnostics: no probe (a hash-derived slot)
-                        gs = (uint32_t)((h >> 17) & a.mask);
-                    } else {
-                        gs = find_or_insert<KW>(a, k, h, gidx, first_ins);
-                    }
-                    if (gs != SLOT_OVF) {
-                        const int ad = lds_adopt<KW>(c, k, h, gs);
-                        accumulate<KW, DBG>(a, c, ad, gs, v, gidx, first_ins);
-                    }
+                if (slot >= 0 && !(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
+                    lds_accumulate<KW, NA>(a, c, slot, v, row_gidx(a, row));
+            }
+            const bool miss = ok && slot < 0 && !(DBG && (a.dbg & 2u));
+            const bool probe = miss && !(DBG && (a.dbg & 256u));
+            uint32_t d[probe_quads<KW>() * 4];
+            if (probe) probe_issue<KW>(a, h, d);
+            if (PIPE && base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
+            if (miss) {
+                // resolve the miss while its row is in registers: finish the HBM probe,
+                // adopt a free LDS entry if the set has one, else hand the updates to the ring
+                const uint64_t gidx = row_gidx(a, row);
+                uint64_t first_ins = 0;
+                if (probe) gs = find_or_insert<KW>(a, k, h, gidx, first_ins, d);
+                else gs = (uint32_t)((h >> 17) & a.mask);   // diagnostics: a hash-derived slot
+                if (gs != SLOT_OVF) {
+                    const int ad = lds_adopt<KW>(c, k, h, gs);
+                    if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, v, gidx);
+                    else ring_push<NA>(a, r, gs, v, gidx, first_ins);
                 }
             }
+            if (!PIPE && base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
         }
-        if constexpr (DBG) {
-            const uint64_t m = __ballot(miss);
-            if (miss) q[(qhead + qn + __popcll(m & lanemask_lt())) % QCAP] = (uint32_t)row;
-            qn += (uint32_t)__popcll(m);
-            if (qn >= 64) {
-                drain_misses<L, DBG>(a, c, q, qhead, 64, lane);
-                qhead = (qhead + 64) % QCAP;
-                qn -= 64;
-            }
-        }
-    }
-    if constexpr (DBG) {
-        while (qn) {
-            const uint32_t cnt = qn < 64 ? qn : 64;
-            drain_misses<L, DBG>(a, c, q, qhead, cnt, lane);
-            qhead = (qhead + cnt) % QCAP;
-            qn -= cnt;
-        }
+        if (lane == 0) atomicAdd(&ring_ctl[2], 1u);
     }
 
     __syncthreads();
@@ -655,12 +745,12 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
         if (gs >= ST_BUSY) continue;
         for (uint32_t x = 0; x < a.naggs; ++x) {
             const uint64_t s = c.agg[x * E + e];
-            if (s) atomicAdd(rec_agg(a, gs, (int)x), (unsigned long long)s);
+            if (s) gadd(rec_agg(a, gs, (int)x), (unsigned long long)s);
         }
         const uint64_t f = c.first[e];
         const uint64_t fi = ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
                                                                         koff_of(KW) + 8)) - 1;
-        if (f < fi) atomicMin(rec_first(a, gs), (unsigned long long)f);
+        if (f < fi) gmin(rec_first(a, gs), (unsigned long long)f);
     }
 }
 
@@ -942,35 +1032,36 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     return IGX_OK;
 }
 
-constexpr size_t GB_LDS_BUDGET = 148 * 1024;   // cache; + 8 KB of miss queues
+constexpr size_t GB_LDS_BUDGET = 140 * 1024;   // cache; + 16 KB of HBM-update ring
 
-template <class L, bool DBG>
+template <class L, bool DBG, int NA>
 static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BUDGET + 8192);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG, NA>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BUDGET + ARING * 16);
         attr = true;
     }
     const size_t entry = 4 + 4 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
     const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, GB_LDS_BUDGET / (8 * entry)));
     const uint32_t E = 8 * nsets;
     a.lds_entries = E;
-    hipLaunchKernelGGL((k_groupby<L, DBG>), dim3(blocks), dim3(GTB), E * entry + (GTB / 64) * QCAP * 4,
-                       ctx->stream, a);
+    hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), E * entry + ARING * 16, ctx->stream, a);
 }
 
 // The diagnostic variants (IGX_GB_DEBUG) are compiled for the top-tcp key only, so the
-// production kernels carry none of their code.
+// production kernels carry none of their code.  Tables with at most two aggregates run a
+// kernel that carries two aggregate slots (fewer registers, fewer loads).
 template <class L>
 static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     if constexpr (std::is_same<L, StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>>::value) {
         if (a.dbg) {
-            launch_gb_as<L, true>(ctx, a, blocks);
+            launch_gb_as<L, true, 2>(ctx, a, blocks);
             return;
         }
     }
-    launch_gb_as<L, false>(ctx, a, blocks);
+    if (a.naggs <= 2) launch_gb_as<L, false, 2>(ctx, a, blocks);
+    else launch_gb_as<L, false, AMAX>(ctx, a, blocks);
 }
 
 extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
@@ -1017,7 +1108,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         a.kmask[w] = 0;
     }
     a.naggs = t->naggs;
-    for (uint32_t x = t->naggs; x < AMAX; ++x) {   // unused slots are still loaded (load_row)
+    for (uint32_t x = t->naggs; x < AMAX; ++x) {   // unused slots are still loaded (issue_row)
         a.vptr[x] = a.cptr[x] = dummy;
         a.vwidth[x] = a.cwidth[x] = 1;
     }
