@@ -87,6 +87,7 @@ struct GbArgs {
     uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
     uint32_t npred;
     uint32_t lds_entries;   // E (8 x sets)
+    uint32_t nl;            // loader waves (1..14)
     // input
     const uint8_t *valid;   // nullable: rows with 0 are skipped (nil / filtered entries)
     const uint8_t *validp;  // valid, or the dummy column when there is none (always loaded)
@@ -176,18 +177,22 @@ struct StaticLayout {
         constexpr int w = Ws[c];
         constexpr int o = off(c);
         const uint8_t *p = a.kcol[c];
+        // the event stream is read once: non-temporal loads, so it does not push the
+        // table's key records out of the caches
         if constexpr (w == 16) {
-            const uint4 q = reinterpret_cast<const uint4 *>(p)[row];
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y; k[o + 2] = q.z; k[o + 3] = q.w;
         } else if constexpr (w == 8) {
-            const uint2 q = reinterpret_cast<const uint2 *>(p)[row];
+            typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+            const v2u q = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y;
         } else if constexpr (w == 4) {
-            k[o] = reinterpret_cast<const uint32_t *>(p)[row];
+            k[o] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p) + row);
         } else if constexpr (w == 2) {
-            k[o] = reinterpret_cast<const uint16_t *>(p)[row];
+            k[o] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(p) + row);
         } else if constexpr (w == 1) {
-            k[o] = p[row];
+            k[o] = __builtin_nontemporal_load(p + row);
         } else {
             static_assert(w % 4 == 0, "key widths other than 1/2 must be multiples of 4");
 #pragma unroll
@@ -386,7 +391,7 @@ __device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, co
 // so each guarded column used to cost a memory round trip of its own; issued together
 // they retire under one wait.
 __device__ __forceinline__ uint32_t ldd(const uint8_t *base, uint64_t off) {
-    return *reinterpret_cast<const uint32_t *>(base + (off & ~3ull));
+    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base + (off & ~3ull)));
 }
 
 // zero-extended value of `width` bytes from the aligned dwords lo (holding its first byte)
@@ -574,14 +579,20 @@ __device__ __forceinline__ void lds_accumulate(const GbArgs &a, const LdsCache<K
 // latency (longer than a load's).  Producer waves therefore push each HBM update as a
 // 16-byte ring entry {slot, lap|what, value} into LDS, and one server wave per workgroup
 // issues them; it loads nothing, so nothing ever waits on their acknowledgement.
-constexpr uint32_t ARING = 1024;            // ring entries (16 B each)
-constexpr uint32_t NPROD = GTB / 64 - 1;    // producer waves; the last wave serves the ring
+constexpr uint32_t ARING = 512;             // HBM-update ring entries (16 B each)
+// Every wait on another wave is bounded: a wait that never ends sets err bit 4
+// (igx_groupby_finalize then fails with IGX_ENOSPC) instead of hanging the GPU.
+constexpr uint32_t SPIN_LIMIT = 1u << 24;
 constexpr uint32_t WHAT_MIN = 15;           // entry kind: atomicMin on `first`
+// wave roles in a workgroup: a.nl loaders stream rows, the next 15 - a.nl waves (probers)
+// resolve LDS misses against HBM, and the last wave serves the HBM-update ring
+constexpr uint32_t NWAVES = GTB / 64;
+constexpr uint32_t NL_DEFAULT = 10;
 
 struct Ring {
     uint2 *lo;            // {slot, (lap << 4) | what}
     uint64_t *hi;         // value
-    uint32_t *ctl;        // [0] tail (reserved), [1] head (consumed), [2] producers done
+    uint32_t *ctl;        // [0] tail (reserved), [1] head (consumed), [2] producer waves done
 };
 
 __device__ __forceinline__ uint32_t ring_lap(uint32_t p) { return (p / ARING + 1u) << 4; }
@@ -607,8 +618,11 @@ __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32
     if ((threadIdx.x & 63) == leader) base = atomicAdd(&r.ctl[0], total);
     base = __shfl(base, (int)leader);
     // wait for room: the server frees entries as it issues them
-    while (base + total - __hip_atomic_load(&r.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > ARING)
+    for (uint32_t spins = 0;
+         base + total - __hip_atomic_load(&r.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > ARING;) {
         __builtin_amdgcn_s_sleep(1);
+        if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); return; }   // never expected: fail, do not hang
+    }
     uint32_t off = base;
     const uint64_t lt = lanemask_lt();
 #pragma unroll
@@ -631,20 +645,23 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
     for (;;) {
         const uint32_t t = __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (t == head) {
-            if (__hip_atomic_load(&r.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == NPROD &&
+            if (__hip_atomic_load(&r.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVES - 1 - a.nl &&
                 __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == head)
                 break;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
+            __builtin_amdgcn_s_sleep(2);   // idle until the probers push or finish (no limit:
+            continue;                      // they bound their own waits)
         }
         const uint32_t n = min(t - head, 64u);
         if (lane < n) {
             const uint32_t p = head + lane;
             uint64_t w;
+            uint32_t spins = 0;
             while (((uint32_t)((w = __hip_atomic_load(reinterpret_cast<uint64_t *>(&r.lo[p % ARING]),
                                                       __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) &
-                    ~15u) != ring_lap(p))
+                    ~15u) != ring_lap(p)) {
                 __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); break; }
+            }
             const uint64_t val = r.hi[p % ARING];
             const uint32_t slot = (uint32_t)w, what = (uint32_t)(w >> 32) & 15u;
             if (!(DBG && (a.dbg & 4u))) {
@@ -657,15 +674,160 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
     }
 }
 
+// ---- loader -> prober hand-off: the miss ring -----------------------------------------
+// A loader that misses the LDS cache does not probe HBM itself (its next row would wait
+// for the probe's round trip): it writes the row's key, hash, index and aggregate values
+// into a ring cell and moves on.  Prober waves take 64 cells at a time and resolve them.
+// Cells follow the bounded MPMC sequence protocol: cell i starts with seq = i; the
+// producer of position p waits for seq == p, fills the cell and sets seq = p + 1; the
+// consumer of p waits for seq == p + 1, reads the cell and sets seq = p + MRING.
+constexpr uint32_t MRING = 256;
+
+template <int KW, int NA>
+struct MissRing {
+    static constexpr int KQ = LdsCache<KW>::KP / 4;          // key quads
+    static constexpr int EQ = KQ + 1 + (NA + 1) / 2;         // + {hash, index} + values
+    uint4 *cell;      // MRING x EQ
+    uint32_t *seq;    // MRING
+    uint32_t *ctl;    // [0] tail (reservations), [1] head (claims), [2] loader waves done
+    uint32_t *err;
+};
+
+template <int KW, int NA>
+__device__ __forceinline__ void miss_push(const MissRing<KW, NA> &m, const uint32_t (&k)[KW], uint64_t h,
+                                          uint64_t gidx, const uint64_t (&v)[NA]) {
+    const uint64_t active = __ballot(true);
+    const uint32_t leader = (uint32_t)__ffsll((long long)active) - 1;
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == leader) base = atomicAdd(&m.ctl[0], (uint32_t)__popcll(active));
+    base = __shfl(base, (int)leader);
+    const uint32_t p = base + (uint32_t)__popcll(active & lanemask_lt());
+    uint32_t *sq = &m.seq[p % MRING];
+    for (uint32_t spins = 0; __hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > SPIN_LIMIT) { atomicOr(m.err, 16u); return; }
+    }
+    uint4 *cl = m.cell + (uint64_t)(p % MRING) * MissRing<KW, NA>::EQ;
+#pragma unroll
+    for (int q = 0; q < MissRing<KW, NA>::KQ; ++q)
+        cl[q] = make_uint4(4 * q + 0 < KW ? k[4 * q + 0] : 0u, 4 * q + 1 < KW ? k[4 * q + 1] : 0u,
+                           4 * q + 2 < KW ? k[4 * q + 2] : 0u, 4 * q + 3 < KW ? k[4 * q + 3] : 0u);
+    cl[MissRing<KW, NA>::KQ] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)gidx, (uint32_t)(gidx >> 32));
+#pragma unroll
+    for (int x = 0; x < NA; x += 2) {
+        const uint64_t v1 = x + 1 < NA ? v[x + 1] : 0ull;
+        cl[MissRing<KW, NA>::KQ + 1 + x / 2] = make_uint4((uint32_t)v[x], (uint32_t)(v[x] >> 32), (uint32_t)v1,
+                                                          (uint32_t)(v1 >> 32));
+    }
+    __hip_atomic_store(sq, p + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Probers resolve PB misses per lane at a time: the LDS cache again (a prober may have
+// adopted the key since), then all PB HBM probes are issued before the first is waited
+// for, then each is finished: adoption of a free LDS entry, or the HBM-update ring.
+constexpr int PB = 1;   // 2 was measured slower (register spills, bigger batches)
+
+template <int KW, int NA>
+struct MissRow {
+    uint32_t k[KW];
+    uint64_t h, gidx;
+    uint64_t v[NA];
+};
+
+template <int KW, int NA>
+__device__ __forceinline__ void read_cell(const MissRing<KW, NA> &m, uint32_t p, MissRow<KW, NA> &x) {
+    const uint4 *cl = m.cell + (uint64_t)(p % MRING) * MissRing<KW, NA>::EQ;
+#pragma unroll
+    for (int q = 0; q < MissRing<KW, NA>::KQ; ++q) {
+        const uint4 t = cl[q];
+        if (4 * q + 0 < KW) x.k[4 * q + 0] = t.x;
+        if (4 * q + 1 < KW) x.k[4 * q + 1] = t.y;
+        if (4 * q + 2 < KW) x.k[4 * q + 2] = t.z;
+        if (4 * q + 3 < KW) x.k[4 * q + 3] = t.w;
+    }
+    const uint4 hq = cl[MissRing<KW, NA>::KQ];
+    x.h = (uint64_t)hq.x | ((uint64_t)hq.y << 32);
+    x.gidx = (uint64_t)hq.z | ((uint64_t)hq.w << 32);
+#pragma unroll
+    for (int i = 0; i < NA; i += 2) {
+        const uint4 t = cl[MissRing<KW, NA>::KQ + 1 + i / 2];
+        x.v[i] = (uint64_t)t.x | ((uint64_t)t.y << 32);
+        if (i + 1 < NA) x.v[i + 1] = (uint64_t)t.z | ((uint64_t)t.w << 32);
+    }
+}
+
+template <int KW, int NA, bool DBG>
+__device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
+                                       const MissRing<KW, NA> &m, uint32_t lane) {
+    for (;;) {
+        uint32_t claim = 0;
+        if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u * PB);
+        claim = __shfl(claim, 0);
+        bool have[PB];
+        MissRow<KW, NA> x[PB];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const uint32_t p = claim + lane + 64u * j;
+            uint32_t *sq = &m.seq[p % MRING];
+            have[j] = true;
+            uint32_t spins = 0;
+            while (__hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p + 1) {
+                if (__hip_atomic_load(&m.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == a.nl) {
+                    if (p >= __hip_atomic_load(&m.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        have[j] = false;   // past the last miss of a finished stream
+                        break;
+                    }
+                    // the loaders are done, so the cell is being written right now: bounded
+                    if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have[j] = false; break; }
+                }
+                __builtin_amdgcn_s_sleep(1);   // waiting for misses: as long as the stream lasts
+            }
+            if (have[j]) {
+                read_cell<KW, NA>(m, p, x[j]);
+                __hip_atomic_store(sq, p + MRING, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // free
+            }
+        }
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < PB; ++j) any = any || have[j];
+        if (__ballot(any) == 0) break;
+        bool probe[PB];
+        uint32_t d[PB][probe_quads<KW>() * 4];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            probe[j] = false;
+            if (have[j]) {
+                uint32_t gs = SLOT_OVF;
+                const int slot = lds_lookup<KW>(c, x[j].k, x[j].h, gs);
+                if (slot >= 0) lds_accumulate<KW, NA>(a, c, slot, x[j].v, x[j].gidx);
+                else probe[j] = true;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+            if (probe[j] && !(DBG && (a.dbg & 256u))) probe_issue<KW>(a, x[j].h, d[j]);
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            if (probe[j]) {
+                uint64_t first_ins = 0;
+                uint32_t gs;
+                if (DBG && (a.dbg & 256u)) gs = (uint32_t)((x[j].h >> 17) & a.mask);   // diagnostics: no probe
+                else gs = find_or_insert<KW>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j]);
+                if (gs != SLOT_OVF) {
+                    const int ad = lds_adopt<KW>(c, x[j].k, x[j].h, gs);
+                    if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x[j].v, x[j].gidx);
+                    else ring_push<NA>(a, r, gs, x[j].v, x[j].gidx, first_ins);
+                }
+            }
+        }
+    }
+}
+
 template <class L, bool DBG, int NA>
 __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     constexpr int KW = L::KW;
-    // PIPE: issue the next row's loads before waiting for this row's probe.  It overlaps
-    // the two round trips but needs a second row of registers: measured slower for the
-    // 18-word top-tcp key (128 VGPRs + scratch spills), so it is off.
-    constexpr bool PIPE = false;
     extern __shared__ uint64_t lds[];
-    __shared__ uint32_t ring_ctl[4];
+    __shared__ uint32_t ring_ctl[8];
     LdsCache<KW> c;
     c.E = a.lds_entries;
     c.nsets = a.lds_entries / 8;
@@ -679,6 +841,11 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     r.hi = reinterpret_cast<uint64_t *>(c.tag + E);   // E is a multiple of 8: 8-B aligned
     r.lo = reinterpret_cast<uint2 *>(r.hi + ARING);
     r.ctl = ring_ctl;
+    MissRing<KW, NA> m;
+    m.cell = reinterpret_cast<uint4 *>(r.lo + ARING);   // 16-B aligned (see launch)
+    m.seq = reinterpret_cast<uint32_t *>(m.cell + MRING * MissRing<KW, NA>::EQ);
+    m.ctl = ring_ctl + 4;
+    m.err = a.err;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         c.st[e] = ST_EMPTY;
@@ -687,13 +854,17 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
         for (uint32_t x = 0; x < a.naggs; ++x) c.agg[x * E + e] = 0;
     }
     for (uint32_t e = threadIdx.x; e < ARING; e += GTB) r.lo[e] = make_uint2(0, 0);
-    if (threadIdx.x < 4) ring_ctl[threadIdx.x] = 0;
+    for (uint32_t e = threadIdx.x; e < MRING; e += GTB) m.seq[e] = e;
+    if (threadIdx.x < 8) ring_ctl[threadIdx.x] = 0;
     __syncthreads();
 
-    if (wave == NPROD) {
+    if (wave == NWAVES - 1) {
         ring_serve<DBG>(a, r, lane);
+    } else if (wave >= a.nl) {
+        prober<KW, NA, DBG>(a, c, r, m, lane);
+        if (lane == 0) atomicAdd(&r.ctl[2], 1u);
     } else {
-        constexpr uint32_t PTB = NPROD * 64;   // rows per workgroup step
+        const uint32_t PTB = a.nl * 64;   // rows per workgroup step
         const uint64_t stride = (uint64_t)gridDim.x * PTB;
         uint64_t base = (uint64_t)blockIdx.x * PTB + wave * 64;
         RowRaw<L, NA> R;
@@ -703,40 +874,24 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
             uint32_t k[KW];
             uint64_t v[NA];
             bool ok = decode_row<L, NA>(a, row, R, k, v) && row < a.n;
+            if (base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
             const uint64_t h = hash_key<KW>(k);
             if (DBG && (a.dbg & 1u)) {   // diagnostics: load + hash only
                 if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live
                 ok = false;
             }
+            if (!ok) continue;
             uint32_t gs = SLOT_OVF;
-            int slot = -1;
-            if (ok) {
-                slot = lds_lookup<KW>(c, k, h, gs);
-                if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
-                if (slot >= 0 && !(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
+            const int slot = lds_lookup<KW>(c, k, h, gs);
+            if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
+            if (slot >= 0) {
+                if (!(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
                     lds_accumulate<KW, NA>(a, c, slot, v, row_gidx(a, row));
+            } else if (!(DBG && (a.dbg & 2u))) {
+                miss_push<KW, NA>(m, k, h, row_gidx(a, row), v);
             }
-            const bool miss = ok && slot < 0 && !(DBG && (a.dbg & 2u));
-            const bool probe = miss && !(DBG && (a.dbg & 256u));
-            uint32_t d[probe_quads<KW>() * 4];
-            if (probe) probe_issue<KW>(a, h, d);
-            if (PIPE && base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
-            if (miss) {
-                // resolve the miss while its row is in registers: finish the HBM probe,
-                // adopt a free LDS entry if the set has one, else hand the updates to the ring
-                const uint64_t gidx = row_gidx(a, row);
-                uint64_t first_ins = 0;
-                if (probe) gs = find_or_insert<KW>(a, k, h, gidx, first_ins, d);
-                else gs = (uint32_t)((h >> 17) & a.mask);   // diagnostics: a hash-derived slot
-                if (gs != SLOT_OVF) {
-                    const int ad = lds_adopt<KW>(c, k, h, gs);
-                    if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, v, gidx);
-                    else ring_push<NA>(a, r, gs, v, gidx, first_ins);
-                }
-            }
-            if (!PIPE && base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
         }
-        if (lane == 0) atomicAdd(&ring_ctl[2], 1u);
+        if (lane == 0) atomicAdd(&m.ctl[2], 1u);
     }
 
     __syncthreads();
@@ -1032,21 +1187,24 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     return IGX_OK;
 }
 
-constexpr size_t GB_LDS_BUDGET = 140 * 1024;   // cache; + 16 KB of HBM-update ring
+constexpr size_t GB_LDS_TOTAL = 156 * 1024;    // cache + the two rings (dynamic LDS)
 
 template <class L, bool DBG, int NA>
 static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG, NA>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BUDGET + ARING * 16);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_TOTAL);
         attr = true;
     }
     const size_t entry = 4 + 4 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
-    const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, GB_LDS_BUDGET / (8 * entry)));
+    const size_t rings = ARING * 16 + MRING * (16 * MissRing<L::KW, NA>::EQ + 4);
+    const size_t budget = GB_LDS_TOTAL - rings;
+    const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, budget / (8 * entry)));
     const uint32_t E = 8 * nsets;
     a.lds_entries = E;
-    hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), E * entry + ARING * 16, ctx->stream, a);
+    const size_t lds = E * entry + ARING * 16 + MRING * (16 * MissRing<L::KW, NA>::EQ + 4);
+    hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), lds, ctx->stream, a);
 }
 
 // The diagnostic variants (IGX_GB_DEBUG) are compiled for the top-tcp key only, so the
@@ -1220,6 +1378,11 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.mask = t->nslots - 1;
     a.max_probe = (uint32_t)std::min<uint64_t>(t->nslots, 1u << 20);
     if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
+    a.nl = NL_DEFAULT;
+    if (const char *d = std::getenv("IGX_GB_LOADERS")) {   // tuning knob
+        const unsigned long v = std::strtoul(d, nullptr, 0);
+        if (v >= 1 && v <= NWAVES - 2) a.nl = (uint32_t)v;
+    }
     a.dbg_cnt = t->dbg_cnt;
     const uint64_t want = (nrows + GTB - 1) / GTB;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus));
