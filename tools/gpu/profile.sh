@@ -11,6 +11,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv 
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o p -- $B > gpurun_out/pmc_write.log 2>&1 || { echo "pmc write failed rc=$?"; tail gpurun_out/pmc_write.log; exit 1; }
 python3 tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --kernel k_groupby \
   --config '{"events": 100000000, "keys": 1000000, "zipf": 1.1}' --out gpurun_out/traffic.json || { echo "traffic parse failed"; exit 1; }
+# (files under profiles/ do not travel back: copy them from gpurun_out/ afterwards)
 cp gpurun_out/traffic.json profiles/$R/traffic.json
 cp gpurun_out/prof/run_kernel_stats.csv profiles/$R/kernel_stats.csv
 timeout -k 10 600 python3 bench.py > gpurun_out/bench_full.log 2>&1 || { echo "bench full failed rc=$?"; tail gpurun_out/bench_full.log; exit 1; }
@@ -21,3 +22,7 @@ cp gpurun_out/profc/run_kernel_stats.csv profiles/$R/configs_kernel_stats.csv
 cat profiles/$R/bench.json | cut -c1-1500
 head -6 profiles/$R/kernel_stats.csv | cut -c1-220
 echo ALL_OK
+# gpurun merges back gpurun_out/ only; locally, after the call:
+#   cp gpurun_out/traffic.json profiles/R/; cp gpurun_out/prof/run_kernel_stats.csv profiles/R/kernel_stats.csv
+#   grep '"metric"' gpurun_out/bench_full.log > profiles/R/bench.json; grep '^{' gpurun_out/configs.log > profiles/R/configs.jsonl
+#   cp gpurun_out/profc/run_kernel_stats.csv profiles/R/configs_kernel_stats.csv
