@@ -276,6 +276,22 @@ int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                   const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
                   uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
 
+/* ---- data movement either side of the path ---------------------------------------------- */
+/* Sender side of the group-by all-to-all: rows (device, nrows x
+ * row_bytes, 4-byte aligned) are copied to out (device, same size) grouped by owner part,
+ * stable within a part; owner = FNV-1a(32) over the first key_bytes/4 u32 words of the row,
+ * mod nparts (1..64).  part_counts (device u64[nparts]) receives the rows per part.  Async. */
+int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32_t row_bytes,
+                       uint32_t key_bytes, uint32_t nparts, uint8_t *out, uint64_t *part_counts);
+/* The step before the path: array-of-structs records on the device (a BPF
+ * map dump of {key, value} structs or perf-ring event structs, e.g. tcptopIpKeyT +
+ * tcptopTrafficT, pkg/gadgets/top/tcp/tracer/tcptop_bpfel_x86.go:15-30) are cut into SoA
+ * columns: field f (byte offset field_off[f], field_width[f] bytes) of record r goes to
+ * out_cols[f] + r * field_width[f].  1..16 fields.  Async. */
+int igx_ingest_aos(igx_ctx *ctx, const void *records, uint64_t nrec, uint32_t rec_bytes,
+                   const uint32_t *field_off, const uint32_t *field_width, uint32_t nfields,
+                   void *const *out_cols);
+
 /* ---- synthetic event generators (device; bit-identical with oracle/igx_oracle.c) ---- */
 int igx_gen_tcp(igx_ctx *ctx, uint64_t seed, uint64_t rank, uint64_t G, uint64_t permA,
                 uint64_t permB, const uint64_t *cdf, uint64_t base, uint64_t n, uint8_t *saddr,

@@ -108,6 +108,9 @@ SIGNATURES = [
     ("igx_np_mark", _I, [_VP, _VP, _VP, _VP, _VP, _U64, _VP]),
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
+    ("igx_partition_rows", _I, [_VP, _VP, _U64, _U32, _U32, _U32, _VP, _VP]),
+    ("igx_ingest_aos", _I, [_VP, _VP, _U64, _U32, C.POINTER(_U32), C.POINTER(_U32), _U32,
+                            C.POINTER(_VP)]),
     ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),
     ("igx_gen_open", _I, [_VP, _U64, _VP, _U64, _U64] + [_VP] * 8),
     ("igx_gen_bio", _I, [_VP, _U64, _VP, _U64, _U64, _U64, _VP, _VP, _VP]),

@@ -1,0 +1,213 @@
+// k_partition.hip -- data movement on either side of the aggregation path.
+//
+// igx_partition_rows: the sender side of the group-by all-to-all:
+//   every packed row (key | partial aggregates | first index) goes to the rank that owns
+//   its key, owner = FNV-1a over the key's u32 words mod nparts (the same value on every
+//   rank and device).  Rows come out grouped by owner, stable within an owner, so one
+//   all-to-all moves them.  Two passes over fixed row chunks: an owner histogram per chunk,
+//   a scan, then a stable scatter (ranks within a wave by ballot over the owners present,
+//   across waves through LDS).
+// igx_ingest_aos: the step before the path: records in the
+//   reference's wire formats -- BPF map dumps of {key struct, value struct}
+//   (`tcptopIpKeyT` 72 B + `tcptopTrafficT` 16 B, `filetopFileId` 24 B, `biotopInfoT` 40 B,
+//   `biolatencyHistKey` 8 B; `*_bpfel_x86.go`) or perf-ring event structs -- are cut into
+//   the SoA columns the kernels stream.  Field = (byte offset in the record, width).
+#include <algorithm>
+#include <vector>
+
+#include "k_common.h"
+
+namespace {
+
+constexpr int PTB = 1024;           // threads per block
+constexpr uint32_t PMAXP = 64;      // parts
+
+__device__ __forceinline__ uint32_t row_owner(const uint8_t *row, uint32_t key_words, uint32_t nparts) {
+    uint32_t h = 0x811C9DC5u;
+    for (uint32_t w = 0; w < key_words; ++w) h = (h ^ reinterpret_cast<const uint32_t *>(row)[w]) * 16777619u;
+    return h % nparts;
+}
+
+__global__ __launch_bounds__(PTB) void k_part_hist(const uint8_t *__restrict__ rows, uint64_t n, uint32_t row_bytes,
+                                                   uint32_t key_words, uint32_t nparts, uint64_t chunk,
+                                                   uint32_t *__restrict__ hist /* [nparts][nblocks] */) {
+    __shared__ uint32_t cnt[PMAXP];
+    if (threadIdx.x < PMAXP) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+    for (uint64_t r = b0 + threadIdx.x; r < b1; r += PTB)
+        atomicAdd(&cnt[row_owner(rows + r * row_bytes, key_words, nparts)], 1u);
+    __syncthreads();
+    if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// exclusive scan of hist in [part][block] order (one block; nparts * nblocks <= 65536)
+__global__ __launch_bounds__(PTB) void k_part_scan(uint32_t *__restrict__ v, uint32_t m, uint32_t nparts,
+                                                   uint32_t nblocks, uint64_t *__restrict__ part_counts) {
+    __shared__ uint32_t part[PTB];
+    const uint32_t per = (m + PTB - 1) / PTB;
+    const uint32_t b = threadIdx.x * per, e = min(m, b + per);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; ++i) s += v[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < PTB; d <<= 1) {
+        const uint32_t x = threadIdx.x >= (uint32_t)d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (uint32_t i = b; i < e; ++i) {
+        const uint32_t c = v[i];
+        v[i] = run;
+        run += c;
+    }
+    __syncthreads();
+    // rows per part = next part's first offset - this part's first offset
+    if (threadIdx.x < nparts) {
+        const uint32_t lo = v[threadIdx.x * nblocks];
+        const uint32_t hi = threadIdx.x + 1 < nparts ? v[(threadIdx.x + 1) * nblocks] : part[PTB - 1];
+        part_counts[threadIdx.x] = hi - lo;
+    }
+}
+
+__global__ __launch_bounds__(PTB) void k_part_scatter(const uint8_t *__restrict__ rows, uint64_t n, uint32_t row_bytes,
+                                                      uint32_t key_words, uint32_t nparts, uint64_t chunk,
+                                                      const uint32_t *__restrict__ off, uint8_t *__restrict__ out) {
+    __shared__ uint32_t base[PMAXP];              // running output offset per part
+    __shared__ uint32_t wcnt[PTB / 64][PMAXP];    // per-wave counts of this tile
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < nparts) base[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+    for (uint64_t t0 = b0; t0 < b1; t0 += PTB) {
+        for (uint32_t i = threadIdx.x; i < (PTB / 64) * PMAXP; i += PTB) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t r = t0 + threadIdx.x;
+        const bool in = r < b1;
+        const uint32_t o = in ? row_owner(rows + r * row_bytes, key_words, nparts) : 0xFFFFFFFFu;
+        // rank within the wave among rows of the same owner (lanes in order)
+        uint32_t rank = 0;
+        uint64_t todo = __ballot(in);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__ffsll((long long)todo) - 1;
+            const uint32_t lo = __shfl(o, (int)leader);
+            const uint64_t m = __ballot(o == lo);
+            if (o == lo) rank = (uint32_t)__popcll(m & lanemask_lt());
+            if (lane == 0) wcnt[wave][lo] = (uint32_t)__popcll(m);
+            todo &= ~m;
+        }
+        __syncthreads();
+        if (in) {
+            uint32_t before = 0;
+            for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][o];
+            const uint64_t dst = (uint64_t)base[o] + before + rank;
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(rows + r * row_bytes);
+            uint32_t *d = reinterpret_cast<uint32_t *>(out + dst * row_bytes);
+            for (uint32_t w = 0; w < row_bytes / 4; ++w) d[w] = src[w];
+        }
+        __syncthreads();
+        if (threadIdx.x < nparts) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < PTB / 64; ++w) tot += wcnt[w][threadIdx.x];
+            base[threadIdx.x] += tot;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- AoS -> SoA -----------------------------------------------------------------------
+struct IngestArgs {
+    const uint8_t *rec;
+    uint64_t n;
+    uint32_t rec_bytes, nf;
+    uint32_t off[16], width[16];
+    uint8_t *dst[16];
+};
+
+// one thread per (record, field); a wave covers 64 consecutive records of one field, so
+// the SoA stores are contiguous; the record reads are strided but every record's line is
+// read by the fields' waves back to back (L2 hits)
+__global__ __launch_bounds__(256) void k_ingest(IngestArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t total = (a.n + 63) / 64 * 64 * a.nf;   // whole 64-record groups
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const uint32_t f = (uint32_t)((i / 64) % a.nf);
+        const uint64_t r = (i / 64 / a.nf) * 64 + (i % 64);
+        if (r >= a.n) continue;
+        const uint8_t *s = a.rec + r * a.rec_bytes + a.off[f];
+        uint8_t *d = a.dst[f] + r * a.width[f];
+        const uint32_t w = a.width[f];
+        if (w == 16 && ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+            *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(s);
+        } else if (w == 8 && ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 7) == 0) {
+            *reinterpret_cast<uint64_t *>(d) = *reinterpret_cast<const uint64_t *>(s);
+        } else if (w == 4 && ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 3) == 0) {
+            *reinterpret_cast<uint32_t *>(d) = *reinterpret_cast<const uint32_t *>(s);
+        } else {
+            for (uint32_t b = 0; b < w; ++b) d[b] = s[b];
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32_t row_bytes,
+                                  uint32_t key_bytes, uint32_t nparts, uint8_t *out, uint64_t *part_counts) {
+    if (!ctx) return IGX_EINVAL;
+    if (nparts == 0 || nparts > PMAXP) return igx_fail(ctx, IGX_EINVAL, "partition: nparts must be 1..%u", PMAXP);
+    if (row_bytes == 0 || row_bytes % 4 || key_bytes % 4 || key_bytes > row_bytes)
+        return igx_fail(ctx, IGX_EINVAL, "partition: rows and keys are whole u32 words");
+    if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "partition: more than 2^32 rows");
+    if (!part_counts || (nrows && (!rows || !out))) return igx_fail(ctx, IGX_EINVAL, "partition: null argument");
+    if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3)
+        return igx_fail(ctx, IGX_EINVAL, "partition: rows must be 4-byte aligned");
+    if (nrows == 0) {
+        IGX_HIP(ctx, hipMemsetAsync(part_counts, 0, nparts * sizeof(uint64_t), ctx->stream));
+        return IGX_OK;
+    }
+    const uint32_t nblocks = (uint32_t)std::min<uint64_t>(std::max(1, ctx->num_cus * 2), (nrows + PTB - 1) / PTB);
+    const uint64_t chunk = (nrows + nblocks - 1) / nblocks;
+    void *scratch;
+    int rc = igx_scratch(ctx, (size_t)nparts * nblocks * 4, &scratch);
+    if (rc) return rc;
+    uint32_t *hist = static_cast<uint32_t *>(scratch);
+    const uint32_t kw = key_bytes / 4;
+    hipLaunchKernelGGL(k_part_hist, dim3(nblocks), dim3(PTB), 0, ctx->stream, rows, nrows, row_bytes, kw, nparts,
+                       chunk, hist);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PTB), 0, ctx->stream, hist, nparts * nblocks, nparts, nblocks,
+                       part_counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3(nblocks), dim3(PTB), 0, ctx->stream, rows, nrows, row_bytes, kw, nparts,
+                       chunk, hist, out);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
+
+extern "C" int igx_ingest_aos(igx_ctx *ctx, const void *records, uint64_t nrec, uint32_t rec_bytes,
+                              const uint32_t *field_off, const uint32_t *field_width, uint32_t nfields,
+                              void *const *out_cols) {
+    if (!ctx) return IGX_EINVAL;
+    if (nfields == 0 || nfields > 16) return igx_fail(ctx, IGX_EINVAL, "ingest: 1..16 fields");
+    if (nrec && (!records || !field_off || !field_width || !out_cols))
+        return igx_fail(ctx, IGX_EINVAL, "ingest: null argument");
+    IngestArgs a{};
+    a.rec = static_cast<const uint8_t *>(records);
+    a.n = nrec;
+    a.rec_bytes = rec_bytes;
+    a.nf = nfields;
+    for (uint32_t f = 0; f < nfields; ++f) {
+        if (field_width[f] == 0 || field_off[f] + field_width[f] > rec_bytes)
+            return igx_fail(ctx, IGX_EINVAL, "ingest: field %u [%u, +%u) outside the %u-byte record", f,
+                            field_off[f], field_width[f], rec_bytes);
+        a.off[f] = field_off[f];
+        a.width[f] = field_width[f];
+        a.dst[f] = static_cast<uint8_t *>(out_cols[f]);
+        if (nrec && !a.dst[f]) return igx_fail(ctx, IGX_EINVAL, "ingest: null output column %u", f);
+    }
+    if (nrec == 0) return IGX_OK;
+    const uint64_t total = (nrec + 63) / 64 * 64 * nfields;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((uint64_t)ctx->num_cus * 8, (total + 255) / 256);
+    hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(256), 0, ctx->stream, a);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}

@@ -62,37 +62,37 @@ def allgather_rows(rows):
     return torch.cat([o[:c] for o, c in zip(outs, counts)])
 
 
-def key_owner(keys, ws):
-    """Owner rank of each packed key row ((n, kb) uint8, kb a multiple of 4): FNV-1a over
-    the key's u32 words, mod world size.  Same value on every rank and device."""
-    torch = torch_mod()
-    n, kb = keys.shape
-    if kb % 4:
-        raise ValueError("packed keys are padded to 4-byte words")
-    w = keys.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-    h = torch.full((n,), 0x811C9DC5, dtype=torch.int64, device=keys.device)
-    for j in range(kb // 4):
-        h = ((h ^ w[:, j]) * 16777619) & 0xFFFFFFFF
-    return (h % ws).to(torch.int64)
+def partition_by_owner(rows, key_bytes, ws):
+    """Group packed rows by the rank that owns their key (igx_partition_rows on the device:
+    FNV-1a over the key's u32 words mod ws, stable).  Returns (rows, counts per rank)."""
+    from . import engine
+    return engine.partition_rows(rows, key_bytes, ws)
 
 
-def exchange_rows(rows, owner):
-    """All-to-all: send row i to rank owner[i]; returns the rows this rank owns (in source
-    rank order, each source's rows in their original order)."""
+def exchange_partitioned(rows, counts):
+    """All-to-all of rows already grouped by destination rank (counts[r] rows for rank r,
+    in rank order).  Returns the rows this rank owns, in source-rank order."""
     d = _dist()
     if d is None or d.get_world_size() == 1:
         return rows
     torch = torch_mod()
-    ws = d.get_world_size()
-    order = torch.argsort(owner, stable=True)
-    send = rows.index_select(0, order).contiguous()
-    send_counts = torch.bincount(owner, minlength=ws).to(torch.int64)
+    send_counts = torch.tensor(counts, dtype=torch.int64, device=rows.device)
     recv_counts = torch.empty_like(send_counts)
     d.all_to_all_single(recv_counts, send_counts)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    rc = recv_counts.tolist()
     out = torch.empty((sum(rc), rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    d.all_to_all_single(out, send, rc, sc)
+    d.all_to_all_single(out, rows.contiguous(), rc, list(counts))
     return out
+
+
+def exchange_rows(rows, key_bytes):
+    """C4 group-by exchange: every partial-group row goes to the rank owning its key."""
+    d = _dist()
+    ws = 1 if d is None else d.get_world_size()
+    if ws == 1:
+        return rows
+    part, counts = partition_by_owner(rows, key_bytes, ws)
+    return exchange_partitioned(part, counts)
 
 
 def unpack_rows(rows, key_widths, naggs):

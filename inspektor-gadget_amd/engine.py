@@ -267,3 +267,38 @@ def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, hist=None)
     ctx.check(ctx.L.igx_hist_log2(ctx.h, ptr(dev), ptr(cont), ptr(delta), n, hd, len(devs),
                                   ncont, divisor, nslots, ptr(hist)))
     return hist
+
+
+# ------------------------------------------------------------------------------------
+# data movement either side of the path
+# ------------------------------------------------------------------------------------
+def partition_rows(rows, key_bytes, nparts):
+    """igx_partition_rows: (n, row_bytes) uint8 device rows grouped by owner part
+    (FNV-1a over the key words mod nparts), stable within a part.  Returns (rows, counts)
+    with counts a host list."""
+    torch = torch_mod()
+    ctx = context()
+    n, rb = rows.shape
+    rows = rows.contiguous()
+    out = torch.empty_like(rows)
+    cnt = torch.zeros(nparts, dtype=torch.int64, device=rows.device)
+    ctx.check(ctx.L.igx_partition_rows(ctx.h, ptr(rows), n, rb, key_bytes, nparts, ptr(out), ptr(cnt)))
+    return out, cnt.cpu().tolist()
+
+
+def ingest_aos(records, n, rec_bytes, fields, device=None):
+    """igx_ingest_aos: records (device uint8, n x rec_bytes) -> {name: SoA column}.
+    fields: [(name, offset, width, dtype)] with dtype a torch dtype (width 1/2/4/8) or
+    None for a byte column (n, width)."""
+    torch = torch_mod()
+    ctx = context()
+    dev = records.device if device is None else device
+    cols = {}
+    for name, off, width, dt in fields:
+        cols[name] = (torch.empty((n, width), dtype=torch.uint8, device=dev) if dt is None
+                      else torch.empty(n, dtype=dt, device=dev))
+    offs = (C.c_uint32 * len(fields))(*[f[1] for f in fields])
+    wids = (C.c_uint32 * len(fields))(*[f[2] for f in fields])
+    outs = (C.c_void_p * len(fields))(*[cols[f[0]].data_ptr() for f in fields])
+    ctx.check(ctx.L.igx_ingest_aos(ctx.h, ptr(records), n, rec_bytes, offs, wids, len(fields), outs))
+    return cols

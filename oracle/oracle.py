@@ -837,3 +837,25 @@ def advisor_policies(events):
                     "spec": spec, "status": {}})
     out.sort(key=lambda p: p["metadata"]["name"])
     return out
+
+
+# ------------------------------------------------------------------------------------
+# multi-GPU exchange reference (dist.py / k_partition.hip)
+# ------------------------------------------------------------------------------------
+def key_owner(keys, ws):
+    """Owner rank of each packed key row ((n, kb) uint8, kb % 4 == 0): FNV-1a(32) over the
+    key's little-endian u32 words, mod ws -- igx_partition_rows' function."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, kb = keys.shape
+    w = keys.view(np.uint32).reshape(n, kb // 4).astype(np.uint64)
+    h = np.full(n, 0x811C9DC5, dtype=np.uint64)
+    for j in range(kb // 4):
+        h = ((h ^ w[:, j]) * np.uint64(16777619)) & np.uint64(0xFFFFFFFF)
+    return (h % np.uint64(ws)).astype(np.int64)
+
+
+def partition_rows(rows, key_bytes, ws):
+    """Stable grouping of rows by key_owner; returns (rows, counts)."""
+    owner = key_owner(np.ascontiguousarray(rows[:, :key_bytes]), ws)
+    order = np.argsort(owner, kind="stable")
+    return np.ascontiguousarray(rows[order]), np.bincount(owner, minlength=ws).tolist()

@@ -71,10 +71,12 @@ def c4_exchange(rank, ws):
                                      base_idx=rank * N)
     rows = torch.from_numpy(rows_of(okeys, oaggs, ofirst))
     kb = okeys.shape[1]
-    owner = D.key_owner(rows[:, :kb], ws)
-    mine = D.exchange_rows(rows, owner)
+    # the device partition (igx_partition_rows) is checked against O.partition_rows in
+    # tests/test_gpu_dist_parts.py; here the oracle's grouping feeds the product's exchange
+    part, counts = O.partition_rows(rows.numpy(), kb, ws)
+    mine = D.exchange_partitioned(torch.from_numpy(part), counts)
     # every received key is owned by this rank
-    check(bool((D.key_owner(mine[:, :kb], ws) == rank).all()), "C4 ownership after all-to-all")
+    check(bool((O.key_owner(mine.numpy()[:, :kb], ws) == rank).all()), "C4 ownership after all-to-all")
     merged = merge_owner(mine.numpy(), kb, 1)
     out = np.array([np.concatenate([np.frombuffer(k, np.uint8), s.view(np.uint8),
                                     np.array([f], np.uint64).view(np.uint8)])
