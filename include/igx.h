@@ -143,6 +143,14 @@ int igx_version(void);
 int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *filter,
                      igx_pred *out, char *errbuf, size_t errlen);
 
+/* Regex rules (IGX_CMP_REGEX, on string columns) run on the device: the pattern is compiled
+ * on the host to a DFA over rune classes with Go regexp semantics (RE2 syntax; UTF-8
+ * decoded like utf8.DecodeRune; unanchored MatchString).  Syntax it does not compile
+ * (\b, \pN, (?m), non-ASCII literals under (?i)) makes igx_filter return IGX_ENOTSUP.
+ * igx_regex_compile_blob exposes the compiled automaton (for tests and tools). */
+int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
+                           size_t *out_len, char *errbuf, size_t errlen);
+
 /* FilterEntries / MatchAll: AND of preds over rows [0,nrows), order-preserving.
  * valid (device, nullable): 0 marks a nil entry (skipped).  out_idx (device) receives
  * the selected row ids; *out_n (device u64) their count.  Asynchronous. */

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "igx_internal.h"
+#include "igx_regex.h"
 
 int igx_fail(igx_ctx *ctx, int code, const char *fmt, ...) {
     if (ctx) {
@@ -98,6 +99,7 @@ extern "C" int igx_close(igx_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (auto &r : ctx->regex) (void)hipFree(r.second);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
     return IGX_OK;
@@ -404,6 +406,42 @@ extern "C" int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, cons
     return IGX_OK;
 }
 
+// compile (once per pattern and context) and upload a regex automaton
+static int regex_device(igx_ctx *ctx, const char *pat, size_t len, const uint8_t **out) {
+    const std::string key(pat, len);
+    auto it = ctx->regex.find(key);
+    if (it == ctx->regex.end()) {
+        RegexDfa dfa;
+        std::string why;
+        const int rc = igx_regex_compile(pat, len, &dfa, &why);
+        if (rc) return igx_fail(ctx, rc, "regular expression %s: %s", key.c_str(), why.c_str());
+        const std::vector<uint8_t> blob = igx_regex_blob(dfa);
+        void *d = nullptr;
+        IGX_HIP(ctx, hipMalloc(&d, blob.size()));
+        const hipError_t e = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return igx_fail(ctx, IGX_EIO, "regex upload: %s", hipGetErrorString(e));
+        }
+        it = ctx->regex.emplace(key, d).first;
+    }
+    *out = static_cast<const uint8_t *>(it->second);
+    return IGX_OK;
+}
+
+extern "C" int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
+                                      size_t *out_len, char *errbuf, size_t errlen) {
+    if (!pattern || !out_len) return IGX_EINVAL;
+    RegexDfa dfa;
+    std::string why;
+    const int rc = igx_regex_compile(pattern, len, &dfa, &why);
+    if (rc) return put_err(errbuf, errlen, rc, why);
+    const std::vector<uint8_t> blob = igx_regex_blob(dfa);
+    *out_len = blob.size();
+    if (out && cap >= blob.size()) std::memcpy(out, blob.data(), blob.size());
+    return IGX_OK;
+}
+
 int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                     uint32_t npreds, DevPreds *out) {
     std::memset(out, 0, sizeof *out);
@@ -412,10 +450,15 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
     for (uint32_t i = 0; i < npreds; ++i) {
         const igx_pred &p = preds[i];
         if (p.col >= ncols) return igx_fail(ctx, IGX_EINVAL, "predicate column %u out of range", p.col);
-        if (p.cmp == IGX_CMP_REGEX) return igx_fail(ctx, IGX_ENOTSUP, "regular-expression filters run on the host");
         if (p.cmp > IGX_CMP_GE) return igx_fail(ctx, IGX_EINVAL, "filter: comparison %u is not a FilterSpec", p.cmp);
         const igx_col &c = cols[p.col];
         DevPred &d = out->p[i];
+        if (p.cmp == IGX_CMP_REGEX) {   // filter.go:146-148: regex rules need a string column
+            if (c.kind != IGX_KIND_BYTES) return igx_fail(ctx, IGX_EINVAL, "regular expression on a non-string column");
+            int rc = regex_device(ctx, reinterpret_cast<const char *>(p.ref), std::min<uint32_t>(p.ref_len, IGX_MAX_REF),
+                                  &d.dfa);
+            if (rc) return rc;
+        }
         d.ptr = static_cast<const uint8_t *>(c.ptr);
         d.width = c.width;
         d.kind = c.kind;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <string>
 
 #include "../../include/igx.h"
@@ -22,6 +23,8 @@ struct igx_ctx {
     // pinned host staging for small readbacks
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
+    // compiled regex automata on the device, by pattern (freed by igx_close)
+    std::map<std::string, void *> regex;
 };
 
 // sets ctx->err and returns code
@@ -49,6 +52,7 @@ struct DevPred {
     const uint8_t *ptr;
     uint32_t width, kind, cmp, negate;
     uint32_t ref_len, pad;
+    const uint8_t *dfa;   // IGX_CMP_REGEX: device regex automaton (igx_regex.h blob)
     uint8_t ref[IGX_MAX_REF];
 };
 struct DevPreds {

@@ -87,8 +87,75 @@ __device__ __forceinline__ int pred_cmp(const DevPred &d, uint64_t row) {
     return a < b ? -1 : (a > b ? 1 : 0);
 }
 
+// regexp.MatchString over a fixed-width string column (filter.go:212-216): the value is
+// the bytes up to the first NUL (gadgets.FromCString), decoded rune by rune like
+// utf8.DecodeRune (an invalid or truncated sequence is one U+FFFD rune of one byte), and
+// run through the host-compiled DFA (igx_regex.cpp) over rune classes.
+struct RegexBlobHdr {
+    uint32_t nstates, ncls, start, bytes, off_bounds, off_flags, off_trans, pad;
+};
+
+__device__ __forceinline__ uint32_t decode_rune(const uint8_t *s, uint32_t n, uint32_t i, uint32_t *len) {
+    const uint32_t c0 = s[i];
+    *len = 1;
+    if (c0 < 0x80) return c0;
+    const uint32_t rem = n - i;
+    if (c0 >= 0xC2 && c0 <= 0xDF && rem >= 2) {
+        const uint32_t c1 = s[i + 1];
+        if ((c1 & 0xC0) == 0x80) { *len = 2; return ((c0 & 0x1F) << 6) | (c1 & 0x3F); }
+    } else if (c0 >= 0xE0 && c0 <= 0xEF && rem >= 3) {
+        const uint32_t c1 = s[i + 1], c2 = s[i + 2];
+        const uint32_t lo = c0 == 0xE0 ? 0xA0 : 0x80, hi = c0 == 0xED ? 0x9F : 0xBF;   // no overlong, no surrogates
+        if (c1 >= lo && c1 <= hi && (c2 & 0xC0) == 0x80) {
+            *len = 3;
+            return ((c0 & 0x0F) << 12) | ((c1 & 0x3F) << 6) | (c2 & 0x3F);
+        }
+    } else if (c0 >= 0xF0 && c0 <= 0xF4 && rem >= 4) {
+        const uint32_t c1 = s[i + 1], c2 = s[i + 2], c3 = s[i + 3];
+        const uint32_t lo = c0 == 0xF0 ? 0x90 : 0x80, hi = c0 == 0xF4 ? 0x8F : 0xBF;
+        if (c1 >= lo && c1 <= hi && (c2 & 0xC0) == 0x80 && (c3 & 0xC0) == 0x80) {
+            *len = 4;
+            return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((c2 & 0x3F) << 6) | (c3 & 0x3F);
+        }
+    }
+    return 0xFFFD;
+}
+
+__device__ __forceinline__ bool regex_match(const uint8_t *blob, const uint8_t *s, uint32_t width) {
+    const RegexBlobHdr *h = reinterpret_cast<const RegexBlobHdr *>(blob);
+    const uint8_t *ascii = blob + sizeof(RegexBlobHdr);
+    const uint32_t *bounds = reinterpret_cast<const uint32_t *>(blob + h->off_bounds);
+    const uint8_t *flags = blob + h->off_flags;
+    const uint16_t *trans = reinterpret_cast<const uint16_t *>(blob + h->off_trans);
+    uint32_t n = 0;
+    while (n < width && s[n]) ++n;
+    uint32_t st = h->start;
+    if (n == 0) return (flags[st] & 5u) != 0;
+    if (flags[st] & 1u) return true;
+    for (uint32_t i = 0; i < n;) {
+        uint32_t len;
+        const uint32_t r = decode_rune(s, n, i, &len);
+        i += len;
+        uint32_t cls;
+        if (r < 128) {
+            cls = ascii[r];
+        } else {   // last class whose first rune <= r
+            uint32_t lo = 0, hi = h->ncls;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (bounds[mid] <= r) lo = mid; else hi = mid;
+            }
+            cls = lo;
+        }
+        st = trans[st * h->ncls + cls];
+        if (flags[st] & 1u) return true;
+    }
+    return (flags[st] & 2u) != 0;
+}
+
 // getComparisonFuncForComparisonType (filter.go:236-263): (field OP ref) != negate
 __device__ __forceinline__ bool pred_match(const DevPred &d, uint64_t row) {
+    if (d.cmp == IGX_CMP_REGEX) return regex_match(d.dfa, d.ptr + row * d.width, d.width) != (d.negate != 0);
     int c = pred_cmp(d, row);
     bool r;
     if (c == 2) r = false;

@@ -1,0 +1,143 @@
+"""The `~` filter's regex compiler (igx_regex.cpp) on the host: the compiled automaton
+(igx_regex_compile_blob), stepped here exactly as the device steps it (k_common.h
+regex_match), must agree with a regular-expression search on every string.  The reference
+is Go's regexp (RE2); the cross-check uses Python's `re` on patterns and texts where the two
+agree (ASCII classes, `$` written as `\\Z` for Python, valid UTF-8 texts), plus known answers
+for Go-specific behaviour: invalid UTF-8 bytes are one U+FFFD rune each, (?i)k matches the
+Kelvin sign, `$` does not match before a final newline."""
+import ctypes as C
+import re
+import struct
+
+import numpy as np
+import pytest
+
+
+def compile_blob(igx, pattern: bytes):
+    L = igx.lib()
+    n = C.c_size_t()
+    err = C.create_string_buffer(256)
+    rc = L.igx_regex_compile_blob(pattern, len(pattern), None, 0, C.byref(n), err, 256)
+    if rc:
+        return rc, err.value.decode()
+    buf = (C.c_uint8 * n.value)()
+    rc = L.igx_regex_compile_blob(pattern, len(pattern), buf, n.value, C.byref(n), err, 256)
+    assert rc == 0
+    return 0, bytes(buf)
+
+
+def decode_rune(s, i):
+    """utf8.DecodeRune: (rune, width); invalid -> (0xFFFD, 1)."""
+    c0 = s[i]
+    rem = len(s) - i
+    if c0 < 0x80:
+        return c0, 1
+    if 0xC2 <= c0 <= 0xDF and rem >= 2 and (s[i + 1] & 0xC0) == 0x80:
+        return ((c0 & 0x1F) << 6) | (s[i + 1] & 0x3F), 2
+    if 0xE0 <= c0 <= 0xEF and rem >= 3:
+        lo, hi = (0xA0 if c0 == 0xE0 else 0x80), (0x9F if c0 == 0xED else 0xBF)
+        if lo <= s[i + 1] <= hi and (s[i + 2] & 0xC0) == 0x80:
+            return ((c0 & 0x0F) << 12) | ((s[i + 1] & 0x3F) << 6) | (s[i + 2] & 0x3F), 3
+    if 0xF0 <= c0 <= 0xF4 and rem >= 4:
+        lo, hi = (0x90 if c0 == 0xF0 else 0x80), (0x8F if c0 == 0xF4 else 0xBF)
+        if lo <= s[i + 1] <= hi and (s[i + 2] & 0xC0) == 0x80 and (s[i + 3] & 0xC0) == 0x80:
+            return (((c0 & 0x07) << 18) | ((s[i + 1] & 0x3F) << 12) | ((s[i + 2] & 0x3F) << 6)
+                    | (s[i + 3] & 0x3F)), 4
+    return 0xFFFD, 1
+
+
+def run_blob(blob, text: bytes, width=None):
+    nstates, ncls, start, nbytes, ob, of, ot, _ = struct.unpack_from("<8I", blob, 0)
+    ascii = blob[32:160]
+    bounds = struct.unpack_from(f"<{ncls}I", blob, ob)
+    flags = blob[of:of + nstates]
+    trans = struct.unpack_from(f"<{nstates * ncls}H", blob, ot)
+    s = text if width is None else text[:width]
+    if b"\0" in s:
+        s = s[:s.index(b"\0")]
+    st = start
+    if not s:
+        return (flags[st] & 5) != 0
+    if flags[st] & 1:
+        return True
+    i = 0
+    while i < len(s):
+        r, w = decode_rune(s, i)
+        i += w
+        if r < 128:
+            cls = ascii[r]
+        else:
+            cls = max(k for k in range(ncls) if bounds[k] <= r)
+        st = trans[st * ncls + cls]
+        if flags[st] & 1:
+            return True
+    return (flags[st] & 2) != 0
+
+
+PATTERNS = ["Demo", "demo", "(?i)demo", "^de", "mo$", "^$", "a*", "x+y", "colou?r", "gr[ae]y", "[^a-z]",
+            r"\d{2,3}", r"^\w+@\w+\.com$", "a|b|cd", "(ab)+c", "(?:foo|bar)baz", "a.c", "a{3}", "a{2,}b",
+            r"\s", r"[\d_-]+$", "(?i)k", "(?s)a.b", "x{0}y", "(a|)b", "[a-c]{1,2}x", r"\.", "é", "^.{2}$",
+            "(?i)[a-f]+z", "(?i:ab)C", "(a*)*b", "^(?:ab|a)(?:bc|c)$", "z?$", "[]a]", "[^]a]"]
+TEXTS = [b"", b"Demo", b"demo", b"a Demo b", b"DEMO", b"dem", b"aaa", b"xxyy", b"color", b"colour",
+         b"grey", b"gray", b"ABC", b"12", b"1234", b"joe@x.com", b"joe@x.comz", b"cd", b"ababc",
+         b"foobaz", b"barbaz", b"abc", b"aXc", b"a\nc", b"aaab", b"a b", b"_-9", b"K", b"k",
+         "é".encode(), "aé".encode(), "éé".encode(), b"y", b"b", b"bx", b"abcx", b".", b"]", b"a",
+         b"abc\n", b"\n"]
+
+
+def py_re(p):
+    """Python rendering of a Go pattern for this test's patterns ($ -> \\Z)."""
+    return re.compile(p.replace("$", r"\Z"))
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_regex_dfa_matches_search(igx, pattern):
+    rc, blob = compile_blob(igx, pattern.encode())
+    assert rc == 0, blob
+    pr = py_re(pattern)
+    for t in TEXTS:
+        want = pr.search(t.decode("utf-8")) is not None
+        assert run_blob(blob, t) == want, (pattern, t)
+
+
+def test_go_specific_known_answers(igx):
+    ok = lambda p, t: run_blob(compile_blob(igx, p)[1], t)   # noqa: E731
+    assert ok(b"(?i)k", "K".encode())            # Kelvin sign folds to k in Go
+    assert ok(b"(?i)s", "ſ".encode())            # long s folds to s
+    assert not ok(b"a$", b"a\n")                      # $ is end of text, not before a final \n
+    assert ok(b"^.$", b"\xff")                        # an invalid byte is one rune
+    assert not ok(b"^..$", b"\xc3")                   # a truncated sequence is one rune
+    assert ok(b"^..$", b"\xc3(")                      # invalid lead byte + '(' = two runes
+    assert ok(b"^.$", "é".encode())                   # one valid 2-byte rune
+    assert ok(b"\xef\xbf\xbd", b"\xfe")               # U+FFFD literal matches an invalid byte
+    assert ok(b"demo", b"demo\0junk")                 # the value ends at the first NUL
+    assert not ok(b"junk", b"demo\0junk")
+
+
+def test_regex_errors_and_unsupported(igx):
+    assert compile_blob(igx, b"(?i)??//{demo")[0] == igx._abi.IGX_EINVAL
+    assert compile_blob(igx, b"a(b")[0] == igx._abi.IGX_EINVAL
+    assert compile_blob(igx, b"[a")[0] == igx._abi.IGX_EINVAL
+    assert compile_blob(igx, b"*a")[0] == igx._abi.IGX_EINVAL
+    for p in (rb"\bfoo", rb"\pL", b"(?m)^a", "(?i)é".encode()):
+        assert compile_blob(igx, p)[0] == igx._abi.IGX_ENOTSUP, p
+
+
+def test_filter_table_regex_rows_on_the_automaton(igx):
+    """filter_test.go:139-143 over the reference table's 5 string values
+    (tests/golden/filter_table.json)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "filter_table.json")))
+    strings = [r["string"] for r in g["records"] if r is not None]
+    for row in g["rows"]:
+        f = row["filter"]
+        if not f.startswith("string:") or "~" not in f or row["error"]:
+            continue
+        rule = f[len("string:"):]
+        neg = rule.startswith("!")
+        pat = rule.lstrip("!")[1:]
+        rc, blob = compile_blob(igx, pat.encode())
+        assert rc == 0
+        cnt = sum(run_blob(blob, s.encode()) != neg for s in strings)
+        assert cnt == row["count"], f
