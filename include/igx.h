@@ -138,8 +138,8 @@ int igx_version(void);
 
 /* ---- filter (host parser + device scan) -------------------------------------------- */
 /* GetFilterFromString: parses "col[:[!][~|>=|>|<=|<]value]".  Host only, no GPU needed.
- * Regex rules parse (and are returned with cmp=IGX_CMP_REGEX) but the device scan rejects
- * them with IGX_ENOTSUP.  errbuf receives the Go error text. */
+ * Regex rules are returned with cmp=IGX_CMP_REGEX and value = the pattern; igx_filter
+ * compiles and runs them (below).  errbuf receives the Go error text. */
 int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *filter,
                      igx_pred *out, char *errbuf, size_t errlen);
 
