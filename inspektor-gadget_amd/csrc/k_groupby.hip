@@ -10,20 +10,24 @@
 // HBM table: S = 2^k slots (S >= 2 x capacity), open addressing with linear probing.
 // Each slot has a key record (KR = 32..256 B, one cache line for every built-in layout):
 //     [0, KOFF)            key words (KW x u32, packed; each key column padded to 4 B)
-//     KOFF                 u64 tag   (hash | 1; 0 = empty)
-//     KOFF + 8             u64 ready (0 = key not yet published, else first_ins + 1:
-//                          the claiming event's index, an upper bound of the group's first)
+//     KOFF                 u64 tag   (hash bits 16..63 | epoch; another epoch = empty)
+//     KOFF + 8             u64 ready (epoch << 48 | first_ins + 1; another epoch = key not
+//                          yet published.  first_ins is the claiming event's index, an
+//                          upper bound of the group's first)
 // and a value record (VR = 8 x 2^m B):  u64 first (first-occurrence event index), then
 // u64 aggregate a at 8 + 8a.  The two are kept apart because 64-bit atomics execute at
 // the memory side and drop their line from L2 (MI355X_MICROARCH.md, store flavours and
 // global atomics): key records are written once per interval and stay L2-resident for
 // the probes, value records only ever receive fire-and-forget atomics.
-// The slot index IS the group id; igx_groupby_finalize lists the occupied slots.
+// The slot index IS the group id; igx_groupby_finalize lists the occupied slots from a
+// bitmap the claimers set (one bit per slot, so the list costs S/8 bytes, not a walk of
+// every key record).  A reset bumps the epoch instead of rewriting the table: records of an
+// older epoch read as empty and the claimer initialises its value record (first =
+// first_ins, aggregates 0) before it publishes `ready`.
 // A new key claims a record with a 64-bit CAS on the tag, writes its key with write-through
 // (sc1) stores and publishes `ready` with an sc1 store after `s_waitcnt vmcnt(0)`; readers
 // load the key record with 16-byte sc1 buffer loads (one round trip) and compare the key
-// in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off table row 1).  No
-// counter is touched per new key.
+// in registers (MI355X_MICROARCH.md §Workgroup dispatch, hand-off table row 1).
 //
 // Each workgroup (1024 threads, one per CU) keeps an LDS key cache: 8-way set associative
 // on the key hash, entries hold the full key, its slot and the workgroup's partial aggregates;
@@ -48,6 +52,10 @@ constexpr int PMAX = 2;   // more predicates: run igx_filter first
 constexpr int GTB = 1024;
 constexpr uint32_t ST_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t ST_BUSY = 0xFFFFFFFEu;
+constexpr uint64_t EP_MAX = 0xFFFF;              // epoch bits in a tag / in `ready`
+constexpr uint64_t READY_IDX = (1ull << 48) - 1;  // `ready` = epoch << 48 | (first_ins + 1)
+
+__device__ __forceinline__ bool ready_ok(uint64_t ready, uint64_t ep) { return (ready >> 48) == ep; }
 
 __host__ __device__ constexpr uint32_t koff_of(int kw) { return (uint32_t)((4 * kw + 7) & ~7); }
 __host__ __device__ constexpr uint32_t pow2_at_least(uint32_t b) {
@@ -100,6 +108,9 @@ struct GbArgs {
     uint32_t krec_total;    // S x KR (< 2^32)
     uint32_t vrec_words;    // VR / 8
     uint32_t *err;
+    uint32_t *occ;          // occupancy bitmap, one bit per slot (set by the claimer)
+    uint64_t ep;            // the interval's epoch (1..EP_MAX): tags and `ready` of older
+                            // epochs read as empty
     uint64_t mask;
     uint32_t max_probe;
     // diagnostics (IGX_GB_DEBUG; compiled into the top-tcp key's debug kernel only):
@@ -287,7 +298,7 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                                                    uint32_t (&d)[probe_quads<KW>() * 4]) {
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
-    const uint64_t tag = h | 1ull;
+    const uint64_t tag = (h & ~EP_MAX) | a.ep;
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     uint64_t s = (h >> 17) & a.mask;
     for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
@@ -296,10 +307,10 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
         uint8_t *r = a.krec + off;
         uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
         uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
-        if (t == 0) {
-            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF), 0ull,
-                                           (unsigned long long)tag);
-            if (old == 0) {
+        if ((t & EP_MAX) != a.ep) {   // empty in this interval (never claimed, or an older epoch's)
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF),
+                                           (unsigned long long)t, (unsigned long long)tag);
+            if (old == t) {
 #pragma unroll
                 for (int w = 0; w < KW; w += 2) {
                     if (w + 1 < KW)
@@ -307,8 +318,13 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                     else
                         st_agent(reinterpret_cast<uint32_t *>(r + 4 * w), k[w]);
                 }
+                // the value record starts at first = first_ins, aggregates 0 (no reset pass)
+                uint64_t *vr = a.vrec + s * a.vrec_words;
+                st_agent(vr, gidx);
+                for (uint32_t x = 1; x < a.vrec_words; ++x) st_agent(vr + x, 0ull);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), gidx + 1);
+                st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), (a.ep << 48) | (gidx + 1));
+                atomicOr(a.occ + (s >> 5), 1u << (s & 31));
                 first_ins = gidx;
                 return (uint32_t)s;
             }
@@ -316,9 +332,9 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
             ready = 0;   // the claimer may still be writing the key
         }
         if (t == tag) {
-            if (!ready) {
+            if (!ready_ok(ready, a.ep)) {
                 uint32_t spins = 0;
-                while (ld_agent(reinterpret_cast<const uint64_t *>(r + KOFF + 8)) == 0) {
+                while (!ready_ok(ld_agent(reinterpret_cast<const uint64_t *>(r + KOFF + 8)), a.ep)) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1u << 22)) {
                         atomicOr(a.err, 2u);
@@ -340,7 +356,7 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                 for (int w = 0; w < KW; ++w) eq = eq && (d[w] == k[w]);
             }
             if (eq) {
-                first_ins = ((uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32)) - 1;
+                first_ins = (((uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32)) & READY_IDX) - 1;
                 return (uint32_t)s;
             }
         }
@@ -903,38 +919,30 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
             if (s) gadd(rec_agg(a, gs, (int)x), (unsigned long long)s);
         }
         const uint64_t f = c.first[e];
-        const uint64_t fi = ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
-                                                                        koff_of(KW) + 8)) - 1;
+        const uint64_t fi = (ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
+                                                                         koff_of(KW) + 8)) & READY_IDX) - 1;
         if (f < fi) gmin(rec_first(a, gs), (unsigned long long)f);
     }
 }
 
-// per-interval reset: tag/ready = 0, first = ~0, aggregates = 0 (keys are left as is)
-__global__ void k_table_reset(uint8_t *krec, uint32_t krec_len, uint32_t koff, uint64_t *vrec, uint32_t vw,
-                              uint64_t ns, uint32_t *err) {
+// Full clear of tags and `ready` (keys and value records are left as is).  Needed only
+// when the epoch counter wraps: every other interval starts by bumping the epoch.
+__global__ void k_table_clear(uint8_t *krec, uint32_t krec_len, uint32_t koff, uint64_t ns) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride)
         *reinterpret_cast<uint4 *>(krec + i * krec_len + koff) = make_uint4(0, 0, 0, 0);
-        uint64_t *v = vrec + i * vw;
-        v[0] = ~0ull;
-        for (uint32_t x = 1; x < vw; ++x) v[x] = 0;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;
 }
 
-// ---- finalize: list the occupied slots in ascending order ----------------------------
-constexpr int CT = 1024;   // slots per compaction tile (256 threads x 4)
+// ---- finalize: list the occupied slots in ascending order, from the occupancy bitmap ----
+constexpr int CT = 256 * 32;   // slots per compaction tile (256 threads x one 32-slot word)
 
-__global__ __launch_bounds__(256) void k_slots_count(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff,
-                                                     uint64_t ns, uint32_t *__restrict__ cnt) {
+__global__ __launch_bounds__(256) void k_slots_count(const uint32_t *__restrict__ occ, uint64_t nwords,
+                                                     uint32_t *__restrict__ cnt) {
     __shared__ uint32_t wc[4];
-    uint32_t c = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t c = i < nwords ? (uint32_t)__popc(occ[i]) : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
-        const bool occ = s < ns && *reinterpret_cast<const uint64_t *>(rec + s * rec_len + koff) != 0;
-        c += __popcll(__ballot(occ));
-    }
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) cnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
@@ -963,49 +971,28 @@ __global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, u
     if (threadIdx.x == 1023) *total = part[1023];
 }
 
-__global__ __launch_bounds__(256) void k_slots_write(const uint8_t *__restrict__ rec, uint32_t rec_len, uint32_t koff,
-                                                     uint64_t ns, const uint32_t *__restrict__ off,
-                                                     uint32_t *__restrict__ out) {
-    __shared__ uint32_t wpre[16];
-    __shared__ uint64_t wmask[16];
+__global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict__ occ, uint64_t nwords,
+                                                     const uint32_t *__restrict__ off, uint32_t *__restrict__ out) {
+    __shared__ uint32_t wsum[4];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t m = i < nwords ? occ[i] : 0u;
+    const uint32_t c = (uint32_t)__popc(m);
+    uint32_t inc = c;   // inclusive scan over the wave
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
-        const bool occ = s < ns && *reinterpret_cast<const uint64_t *>(rec + s * rec_len + koff) != 0;
-        const uint64_t m = __ballot(occ);
-        if (lane == 0) wmask[j * 4 + wave] = m;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += x;
     }
+    if (lane == 63) wsum[wave] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t r = 0;
-        for (int w = 0; w < 16; ++w) {
-            wpre[w] = r;
-            r += __popcll(wmask[w]);
-        }
-    }
-    __syncthreads();
-    const uint32_t base = off[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t w = j * 4 + wave;
-        const uint64_t m = wmask[w];
-        if ((m >> lane) & 1ull) {
-            const uint64_t s = (uint64_t)blockIdx.x * CT + j * 256 + threadIdx.x;
-            out[base + wpre[w] + __popcll(m & lanemask_lt())] = (uint32_t)s;
-        }
-    }
-}
-
-// first = min(value record's first, key record's first_ins) for every listed group
-__global__ void k_fold_first(const uint8_t *__restrict__ krec, uint32_t krec_len, uint32_t koff,
-                             uint64_t *__restrict__ vrec, uint32_t vw, const uint32_t *__restrict__ groups,
-                             uint64_t ng) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ng; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t g = groups[i];
-        const uint64_t fi = *reinterpret_cast<const uint64_t *>(krec + (uint64_t)g * krec_len + koff + 8) - 1;
-        uint64_t *f = vrec + (uint64_t)g * vw;
-        if (fi < *f) *f = fi;
+    uint32_t base = off[blockIdx.x] + inc - c;
+    for (uint32_t w = 0; w < wave; ++w) base += wsum[w];
+    const uint32_t s0 = (uint32_t)(i * 32);
+    while (m) {
+        const uint32_t bit = (uint32_t)__ffs(m) - 1;
+        out[base++] = s0 + bit;
+        m &= m - 1;
     }
 }
 
@@ -1059,6 +1046,9 @@ struct igx_table {
     uint32_t *err = nullptr;
     uint32_t *groups = nullptr;  // occupied slots after finalize
     uint32_t *tile_cnt = nullptr;
+    uint32_t *occ = nullptr;     // occupancy bitmap (nslots bits)
+    uint64_t occ_words = 0;
+    uint64_t ep = 0;             // current epoch (1..EP_MAX)
     uint64_t *n_groups = nullptr;
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
@@ -1152,6 +1142,8 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMalloc(&t->err, 64);
     if (e == hipSuccess) e = hipMalloc(&t->groups, ns * 4);
     if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
+    t->occ_words = (ns + 31) / 32;
+    if (e == hipSuccess) e = hipMalloc(&t->occ, t->occ_words * 4);
     if (e == hipSuccess) e = hipMalloc(&t->n_groups, 64);
     if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
     if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream);
@@ -1166,9 +1158,16 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
 extern "C" int igx_groupby_reset(igx_table *t) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    hipLaunchKernelGGL(k_table_reset, dim3(2048), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff, t->vrec,
-                       t->vrec_len / 8, t->nslots, t->err);
-    IGX_HIP(ctx, hipGetLastError());
+    // A new interval is a new epoch: records of older epochs read as empty and a claimer
+    // initialises its value record, so only the bitmap and the error word are cleared.
+    if (++t->ep > EP_MAX) {
+        hipLaunchKernelGGL(k_table_clear, dim3(2048), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
+                           t->nslots);
+        IGX_HIP(ctx, hipGetLastError());
+        t->ep = 1;
+    }
+    IGX_HIP(ctx, hipMemsetAsync(t->occ, 0, t->occ_words * 4, ctx->stream));
+    IGX_HIP(ctx, hipMemsetAsync(t->err, 0, 4, ctx->stream));
     t->host_groups = 0;
     return IGX_OK;
 }
@@ -1181,6 +1180,7 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->err);
     (void)hipFree(t->groups);
     (void)hipFree(t->tile_cnt);
+    (void)hipFree(t->occ);
     (void)hipFree(t->n_groups);
     (void)hipFree(t->dbg_cnt);
     delete t;
@@ -1375,6 +1375,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.krec_total = (uint32_t)(t->nslots * t->krec_len);
     a.vrec_words = t->vrec_len / 8;
     a.err = t->err;
+    a.occ = t->occ;
+    a.ep = t->ep;
     a.mask = t->nslots - 1;
     a.max_probe = (uint32_t)std::min<uint64_t>(t->nslots, 1u << 20);
     if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
@@ -1418,11 +1420,11 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     const uint64_t tiles = (t->nslots + CT - 1) / CT;
-    hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
-                       t->nslots, t->tile_cnt);
+    hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
+                       t->tile_cnt);
     hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups);
-    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
-                       t->nslots, t->tile_cnt, t->groups);
+    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
+                       t->tile_cnt, t->groups);
     IGX_HIP(ctx, hipGetLastError());
     uint64_t *h;
     int rc = igx_pinned(ctx, 16, reinterpret_cast<void **>(&h));
@@ -1433,12 +1435,6 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     const uint64_t ng = h[0];
     const uint32_t err = reinterpret_cast<uint32_t *>(h)[2];
     t->host_groups = ng;
-    if (ng && !err) {
-        const uint32_t fb = (uint32_t)std::min<uint64_t>(4096, (ng + 255) / 256);
-        hipLaunchKernelGGL(k_fold_first, dim3(fb), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff, t->vrec,
-                           t->vrec_len / 8, t->groups, ng);
-        IGX_HIP(ctx, hipGetLastError());
-    }
     if (view) {
         view->n_groups = ng;
         view->n_slots = t->nslots;

@@ -165,6 +165,40 @@ def test_fused_predicates_signed_and_chunks(oracle, E, H, igx, torch):
     tab.destroy()
 
 
+def test_intervals_and_epoch_wrap(oracle, E, H, igx, torch):
+    """Reset = a new epoch (records of older epochs read as empty, claimers re-initialise
+    their value records).  Two streams with overlapping key sets alternate across the
+    65535-epoch wrap, where reset falls back to a full clear."""
+    A = igx._abi
+    n = 300_000
+    evs = []
+    for seed, G in ((0xA1, 3000), (0xB2, 6000)):
+        ev_h = oracle.gen_tcp(seed, 0, G, oracle.zipf_cdf(G, 1.0), 0, n)
+        o = oracle.groupby(oracle.pack_cols(ev_h, ("pid",)), [{"kind": "count"}, {"kind": "sum", "val": ev_h["size"]}])
+        evs.append(({k: H.to_device(ev_h[k]) for k in ("pid", "size")}, o))
+    aggs = [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0), A.Agg(A.AGG_SUM, 1, A.NO_COL, 8, 0)]
+    tab = E.Table([4], aggs, 8192)
+
+    def interval(which):
+        ev, o = evs[which]
+        tab.update([ev["pid"], ev["size"]], [0], n, 0)
+        _check(E, H, tab, [4], *o)
+
+    interval(0)                       # epoch 1
+    tab.reset()
+    interval(1)                       # epoch 2
+    for _ in range(65532):
+        tab.reset()
+    assert tab.finalize()["n_groups"] == 0
+    tab.reset()
+    interval(0)                       # epoch 65535
+    tab.reset()
+    interval(1)                       # wrapped: full clear, epoch 1
+    tab.reset()
+    interval(0)                       # epoch 2
+    tab.destroy()
+
+
 def test_capacity_overflow_is_reported(oracle, E, H, igx, torch):
     A = igx._abi
     G, n = 5000, 200_000
