@@ -107,21 +107,52 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
     payload[i] = (uint32_t)src;
 }
 
-// per-word AND / OR over all rows -> res[2*w] (and), res[2*w+1] (or)
+// per-word AND / OR over all rows -> res[2*w] (and), res[2*w+1] (or).  16-byte loads, four
+// in flight per lane, one atomic pair per workgroup and word.
 __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words, uint64_t n,
                                               uint64_t stride, uint32_t *__restrict__ res) {
+    __shared__ uint32_t red[2][TB / 64];
     const uint32_t w = blockIdx.y;
+    const uint32_t *col = words + (uint64_t)w * stride;   // stride is a multiple of 64 rows
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(col);
+    const uint64_t n4 = n / 4;
     uint32_t va = 0xFFFFFFFFu, vo = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TB) {
-        uint32_t v = words[w * stride + i];
-        va &= v;
-        vo |= v;
+    const uint64_t step = (uint64_t)gridDim.x * TB;
+    uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    for (; i + 3 * step < n4; i += 4 * step) {
+        uint4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = v4[i + j * step];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            va &= q[j].x & q[j].y & q[j].z & q[j].w;
+            vo |= q[j].x | q[j].y | q[j].z | q[j].w;
+        }
+    }
+    for (; i < n4; i += step) {
+        const uint4 q = v4[i];
+        va &= q.x & q.y & q.z & q.w;
+        vo |= q.x | q.y | q.z | q.w;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {   // rows past the last whole quad
+        const uint32_t x = col[n4 * 4 + threadIdx.x];
+        va &= x;
+        vo |= x;
     }
     for (int o = 32; o > 0; o >>= 1) {
         va &= __shfl_xor(va, o);
         vo |= __shfl_xor(vo, o);
     }
     if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = va;
+        red[1][threadIdx.x >> 6] = vo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 1; j < TB / 64; ++j) {
+            va &= red[0][j];
+            vo |= red[1][j];
+        }
         atomicAnd(&res[2 * w], va);
         atomicOr(&res[2 * w + 1], vo);
     }
@@ -454,7 +485,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
     hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
     hipLaunchKernelGGL(k_init_andor, dim3(1), dim3(TB), 0, ctx->stream, res, KW);
-    const uint32_t ablocks = (uint32_t)std::min<uint64_t>(64, (nrows + TB - 1) / TB);
+    const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, nrows / (4 * TB)));
     hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, res);
     uint32_t *hres;
     rc = igx_pinned(ctx, KW * 8, reinterpret_cast<void **>(&hres));
