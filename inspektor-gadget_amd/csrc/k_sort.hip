@@ -107,10 +107,11 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
     payload[i] = (uint32_t)src;
 }
 
-// per-word AND / OR over all rows -> res[2*w] (and), res[2*w+1] (or).  16-byte loads, four
-// in flight per lane, one atomic pair per workgroup and word.
+// per-word AND / OR over all rows -> part[(w * gridDim.x + block) * 2 + {0: and, 1: or}].
+// 16-byte loads, four in flight per lane; partials, not atomics: the words' results share
+// one line, and same-line atomics from every workgroup serialise at the memory side.
 __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words, uint64_t n,
-                                              uint64_t stride, uint32_t *__restrict__ res) {
+                                              uint64_t stride, uint32_t *__restrict__ part) {
     __shared__ uint32_t red[2][TB / 64];
     const uint32_t w = blockIdx.y;
     const uint32_t *col = words + (uint64_t)w * stride;   // stride is a multiple of 64 rows
@@ -153,16 +154,37 @@ __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words
             va &= red[0][j];
             vo |= red[1][j];
         }
-        atomicAnd(&res[2 * w], va);
-        atomicOr(&res[2 * w + 1], vo);
+        part[2 * ((uint64_t)w * gridDim.x + blockIdx.x)] = va;
+        part[2 * ((uint64_t)w * gridDim.x + blockIdx.x) + 1] = vo;
     }
 }
 
-__global__ __launch_bounds__(TB) void k_init_andor(uint32_t *res, uint32_t nw) {
-    uint32_t t = threadIdx.x;
-    if (t < nw) {
-        res[2 * t] = 0xFFFFFFFFu;
-        res[2 * t + 1] = 0;
+// res[2*w], res[2*w+1] = AND / OR of word w's nb partials (one workgroup per word)
+__global__ __launch_bounds__(TB) void k_andor_final(const uint32_t *__restrict__ part, uint32_t nb,
+                                                    uint32_t *__restrict__ res) {
+    __shared__ uint32_t red[2][TB / 64];
+    const uint32_t w = blockIdx.x;
+    uint32_t va = 0xFFFFFFFFu, vo = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += TB) {
+        va &= part[2 * ((uint64_t)w * nb + b)];
+        vo |= part[2 * ((uint64_t)w * nb + b) + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        va &= __shfl_xor(va, o);
+        vo |= __shfl_xor(vo, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = va;
+        red[1][threadIdx.x >> 6] = vo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 1; j < TB / 64; ++j) {
+            va &= red[0][j];
+            vo |= red[1][j];
+        }
+        res[2 * w] = va;
+        res[2 * w + 1] = vo;
     }
 }
 
@@ -468,7 +490,8 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const size_t pay_b = igx_align(stride * 4, 256);
     const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
                           igx_align(((size_t)256 * nblocks + SCAN_CHUNK - 1) / SCAN_CHUNK * 4, 256);
-    const size_t res_b = igx_align((size_t)KW * 8, 256);
+    constexpr uint32_t ANDOR_BLOCKS = 256;
+    const size_t res_b = igx_align((size_t)KW * 8, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     void *s;
@@ -484,9 +507,10 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
 
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
     hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
-    hipLaunchKernelGGL(k_init_andor, dim3(1), dim3(TB), 0, ctx->stream, res, KW);
-    const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, nrows / (4 * TB)));
-    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, res);
+    const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
+    uint32_t *apart = res + igx_align((size_t)KW * 2, 64);
+    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart);
+    hipLaunchKernelGGL(k_andor_final, dim3(KW), dim3(TB), 0, ctx->stream, apart, ablocks, res);
     uint32_t *hres;
     rc = igx_pinned(ctx, KW * 8, reinterpret_cast<void **>(&hres));
     if (rc) return rc;
