@@ -217,11 +217,14 @@ typedef struct {
 /* IGX_TSRC_CONST: a column that holds the same value for every group (e.g. the
  * CommonData enrichment strings when nothing enriches).  Go still runs a SliceStable pass
  * for it, so it orders nothing but its '-' flips the tie parity. */
-enum igx_tsrc { IGX_TSRC_AGG = 0, IGX_TSRC_FIRST = 1, IGX_TSRC_KEY = 2, IGX_TSRC_CONST = 3 };
+/* IGX_TSRC_IPTEXT: the text of a 16-byte address in the key (offset) under the u16 family
+ * in the key (index = its byte offset), as IPStringFromBytes renders it (helpers.go:111-120,
+ * top/tcp/tracer/tracer.go:199-206): the Saddr / Daddr string columns of the Stats rows. */
+enum igx_tsrc { IGX_TSRC_AGG = 0, IGX_TSRC_FIRST = 1, IGX_TSRC_KEY = 2, IGX_TSRC_CONST = 3, IGX_TSRC_IPTEXT = 4 };
 typedef struct {
     uint32_t src;    /* enum igx_tsrc */
-    uint32_t index;  /* aggregate index (IGX_TSRC_AGG) */
-    uint32_t offset; /* byte offset in the packed key (IGX_TSRC_KEY) */
+    uint32_t index;  /* aggregate index (IGX_TSRC_AGG); family byte offset (IGX_TSRC_IPTEXT) */
+    uint32_t offset; /* byte offset in the packed key (IGX_TSRC_KEY, IGX_TSRC_IPTEXT) */
     uint32_t width;  /* bytes (IGX_TSRC_KEY) */
     uint32_t kind;   /* enum igx_kind (IGX_TSRC_KEY) */
     uint32_t desc;   /* '-' prefix */
@@ -280,6 +283,16 @@ int igx_np_mark(igx_ctx *ctx, const uint8_t *typ, const uint8_t *pkt, const uint
  * ndev == 0 is the shipped gadget's keying (no targ_per_disk / targ_per_flag): every row
  * is device index 0 and dev may be NULL.  cont may be NULL (ncont must then be 1).
  * hist (device u32, max(ndev,1)*ncont*nslots) accumulates.  Async. */
+/* IPStringFromBytes (pkg/gadgets/helpers.go:111-120) for n rows: addr (16 bytes at row *
+ * addr_stride) rendered as netip.AddrFrom16(...).String() when the u16 family at row *
+ * family_stride is AF_INET6 (10), else netip.AddrFrom4(addr[0:4]).String().  out (device,
+ * 8-byte aligned) receives n x IGX_IPTEXT_WIDTH bytes, each text zero-padded, so byte order
+ * of two rows is Go's string order.  rowmap (device, nullable): row r reads row rowmap[r].
+ * Asynchronous. */
+#define IGX_IPTEXT_WIDTH 40
+int igx_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t addr_stride, const uint8_t *family,
+                uint32_t family_stride, const uint32_t *rowmap, uint64_t n, uint8_t *out);
+
 int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                   const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
                   uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);

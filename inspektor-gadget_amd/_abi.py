@@ -57,7 +57,8 @@ class TableView(C.Structure):
                 ("d_n_groups", C.c_void_p)]
 
 
-TSRC_AGG, TSRC_FIRST, TSRC_KEY, TSRC_CONST = 0, 1, 2, 3
+TSRC_AGG, TSRC_FIRST, TSRC_KEY, TSRC_CONST, TSRC_IPTEXT = 0, 1, 2, 3, 4
+IPTEXT_WIDTH = 40
 
 
 class TSortKey(C.Structure):
@@ -103,6 +104,7 @@ SIGNATURES = [
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
     ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
+    ("igx_ip_text", _I, [_VP, _VP, _U32, _VP, _U32, _VP, _U64, _VP]),
     ("igx_groupby_reset", _I, [_VP]),
     ("igx_groupby_destroy", _I, [_VP]),
     ("igx_groupby_debug_counts", _I, [_VP, _VP]),

@@ -520,7 +520,7 @@ extern "C" int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, cons
 
 static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                        uint64_t nrows, const uint64_t *pos, const uint8_t *valid, uint32_t *out, uint32_t limit,
-                       const uint32_t *rowmap, uint32_t pos_stride = 8) {
+                       const uint32_t *rowmap, uint32_t pos_stride = 8, uint32_t direct_mask = 0) {
     if (!ctx) return IGX_EINVAL;
     if (nrows == 0) return IGX_OK;                          // sort.go:36-38
     if (!out) return igx_fail(ctx, IGX_EINVAL, "sort: null output");
@@ -538,6 +538,7 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
         p.width = k.width;
         p.kind = k.kind;
         p.stride = strides ? strides[i] : k.width;
+        p.direct = (direct_mask >> i) & 1u;
         if (!p.ptr) return igx_fail(ctx, IGX_EINVAL, "sort: key %u has no column", i);
         if (k.kind == IGX_KIND_BYTES) {
             p.words = (k.width + 3) / 4;
@@ -563,8 +564,18 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
 
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
-                     uint32_t limit, uint32_t *out) {
-    return sort_common(ctx, keys, strides, nkeys, nrows, pos, nullptr, out, limit, rowmap, pos_stride);
+                     uint32_t limit, uint32_t *out, uint32_t direct_mask) {
+    return sort_common(ctx, keys, strides, nkeys, nrows, pos, nullptr, out, limit, rowmap, pos_stride, direct_mask);
+}
+
+extern "C" int igx_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t addr_stride, const uint8_t *family,
+                           uint32_t family_stride, const uint32_t *rowmap, uint64_t n, uint8_t *out) {
+    if (!ctx) return IGX_EINVAL;
+    if (n && (!addr || !family || !out)) return igx_fail(ctx, IGX_EINVAL, "ip_text: null argument");
+    if (n && (addr_stride < 16 || family_stride < 2))
+        return igx_fail(ctx, IGX_EINVAL, "ip_text: strides must cover 16-byte addresses and 2-byte families");
+    if (reinterpret_cast<uintptr_t>(out) % 8) return igx_fail(ctx, IGX_EINVAL, "ip_text: output not 8-byte aligned");
+    return launch_ip_text(ctx, addr, addr_stride, family, family_stride, rowmap, n, out);
 }
 
 extern "C" int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,

@@ -71,7 +71,11 @@ int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64
 struct SortPlanKey {
     const uint8_t *ptr;
     uint32_t width, kind, desc_eff, words, stride;
+    uint32_t direct;   // row r reads this key at r even when a rowmap is given
 };
+// IP text of n rows (rowmap nullable) -> out, n x IGX_IPTEXT_WIDTH bytes (k_sort.hip)
+int launch_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t astride, const uint8_t *fam, uint32_t fstride,
+                   const uint32_t *rowmap, uint64_t n, uint8_t *out);
 // rowmap (device, nullable): row r reads its keys / pos at rowmap[r] and the permutation
 // reports rowmap[r] (used to sort a table's groups through its slot list).
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
@@ -81,7 +85,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
 // closed-form planning + launch (igx_host.cpp); strides per key (nullable = widths)
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
-                     uint32_t limit, uint32_t *out);
+                     uint32_t limit, uint32_t *out, uint32_t direct_mask = 0);
 
 int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                      const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,

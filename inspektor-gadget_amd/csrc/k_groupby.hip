@@ -1072,6 +1072,8 @@ struct igx_table {
     uint64_t *n_groups = nullptr;
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
+    uint8_t *text[8] = {};       // IP text of the groups, per IGX_TSRC_IPTEXT sort key
+    uint64_t text_rows[8] = {};
 };
 
 // compile-time key layouts: the reference's BPF key structs + single-column keys
@@ -1203,6 +1205,7 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->occ);
     (void)hipFree(t->n_groups);
     (void)hipFree(t->dbg_cnt);
+    for (auto *p : t->text) (void)hipFree(p);
     delete t;
     return IGX_OK;
 }
@@ -1504,6 +1507,7 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
     if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "groupby_sort: more than 8 keys");
     igx_sortkey sk[8];
     uint32_t strides[8];
+    uint32_t direct = 0;
     for (uint32_t i = 0; i < nkeys; ++i) {
         const igx_tsortkey &q = keys[i];
         sk[i] = igx_sortkey{};
@@ -1529,12 +1533,33 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
             strides[i] = t->krec_len;
             sk[i].width = q.width;
             sk[i].kind = q.kind;
+        } else if (q.src == IGX_TSRC_IPTEXT) {
+            // a Stats string column made from key bytes: render the groups' texts (in slot-list
+            // order) and sort them as strings
+            if (q.offset + 16 > t->key_words * 4 || q.index + 2 > t->key_words * 4)
+                return igx_fail(ctx, IGX_EINVAL, "groupby_sort: address / family bytes out of range");
+            const uint64_t ng = std::max<uint64_t>(t->host_groups, 1);
+            if (t->text_rows[i] < ng) {
+                (void)hipFree(t->text[i]);
+                t->text[i] = nullptr;
+                t->text_rows[i] = 0;
+                IGX_HIP(ctx, hipMalloc(&t->text[i], ng * IGX_IPTEXT_WIDTH));
+                t->text_rows[i] = ng;
+            }
+            const int rc = launch_ip_text(ctx, t->krec + q.offset, t->krec_len, t->krec + q.index, t->krec_len,
+                                          t->groups, t->host_groups, t->text[i]);
+            if (rc) return rc;
+            sk[i].ptr = t->text[i];
+            strides[i] = IGX_IPTEXT_WIDTH;
+            sk[i].width = IGX_IPTEXT_WIDTH;
+            sk[i].kind = IGX_KIND_BYTES;
+            direct |= 1u << i;
         } else {
             return igx_fail(ctx, IGX_EINVAL, "groupby_sort: bad source");
         }
     }
     return sort_common_rows(ctx, sk, strides, nkeys, t->host_groups, t->groups,
-                            t->vrec, t->vrec_len, k, out_slots);
+                            t->vrec, t->vrec_len, k, out_slots, direct);
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.

@@ -31,7 +31,7 @@ constexpr int MAXW = 80;          // composed words (<= 8 keys x 64-byte strings
 
 struct ComposeArgs {
     const uint8_t *ptr[8];
-    uint32_t width[8], kind[8], desc[8], words[8], rstride[8];
+    uint32_t width[8], kind[8], desc[8], words[8], rstride[8], direct[8];   // direct: read at i, not rowmap[i]
     uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
     const uint64_t *pos;
     const uint8_t *valid;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
             continue;
         }
         const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
-        const uint8_t *p = a.ptr[k] + src * a.rstride[k];
+        const uint8_t *p = a.ptr[k] + (a.direct[k] ? i : src) * a.rstride[k];
         if (a.kind[k] == IGX_KIND_BYTES) {
             for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
@@ -451,7 +451,106 @@ __global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W,
     }
 }
 
+// ---- IP address text (gadgets.IPStringFromBytes, pkg/gadgets/helpers.go:111-120) ----------
+// netip.AddrFrom4(b[0:4]).String() when family != AF_INET6, else netip.AddrFrom16(b).String():
+// dotted decimal; IPv4-mapped as "::ffff:a.b.c.d"; otherwise RFC 5952 hex groups without
+// leading zeros, the first longest run of >= 2 zero groups written "::" (Go netip appendTo6).
+// Rows are rendered zero-padded to IGX_IPTEXT_WIDTH bytes, so a byte compare of two rows is
+// Go's string compare of the two texts.
+constexpr int IPW = IGX_IPTEXT_WIDTH;
+static_assert(IPW % 8 == 0, "rows are written as 8-byte words");
+
+__device__ __forceinline__ int ip_put_dec(uint8_t *o, int p, uint32_t v) {
+    if (v >= 100) o[p++] = (uint8_t)('0' + v / 100);
+    if (v >= 10) o[p++] = (uint8_t)('0' + (v / 10) % 10);
+    o[p++] = (uint8_t)('0' + v % 10);
+    return p;
+}
+
+__device__ __forceinline__ int ip_put_hex(uint8_t *o, int p, uint32_t v) {
+    bool started = false;
+    for (int sh = 12; sh >= 0; sh -= 4) {
+        const uint32_t d = (v >> sh) & 15u;
+        if (d || started || sh == 0) {
+            o[p++] = (uint8_t)(d < 10 ? '0' + d : 'a' + d - 10);
+            started = true;
+        }
+    }
+    return p;
+}
+
+__device__ __forceinline__ int ip_put4(uint8_t *o, int p, const uint8_t *b) {
+    for (int j = 0; j < 4; ++j) {
+        if (j) o[p++] = '.';
+        p = ip_put_dec(o, p, b[j]);
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(TB) void k_ip_text(const uint8_t *__restrict__ addr, uint32_t astride,
+                                                const uint8_t *__restrict__ fam, uint32_t fstride,
+                                                const uint32_t *__restrict__ rowmap, uint64_t n,
+                                                uint8_t *__restrict__ out) {
+    __shared__ uint2 buf[TB][IPW / 8];   // one text per thread
+    const uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    uint8_t *o = reinterpret_cast<uint8_t *>(buf[threadIdx.x]);
+    for (int j = 0; j < IPW / 8; ++j) buf[threadIdx.x][j] = make_uint2(0, 0);
+    if (i < n) {
+        const uint64_t src = rowmap ? rowmap[i] : i;
+        uint8_t b[16];
+        for (int j = 0; j < 16; ++j) b[j] = addr[src * astride + j];
+        const uint32_t f = (uint32_t)fam[src * fstride] | ((uint32_t)fam[src * fstride + 1] << 8);
+        int p = 0;
+        if (f != 10) {                                   // ipType 4 (tracer.go:199-203)
+            p = ip_put4(o, p, b);
+        } else {
+            bool mapped = b[10] == 0xFF && b[11] == 0xFF;
+            for (int j = 0; j < 10; ++j) mapped = mapped && b[j] == 0;
+            if (mapped) {
+                const char pre[7] = {':', ':', 'f', 'f', 'f', 'f', ':'};
+                for (int j = 0; j < 7; ++j) o[p++] = (uint8_t)pre[j];
+                p = ip_put4(o, p, b + 12);
+            } else {
+                uint32_t g[8];
+                for (int j = 0; j < 8; ++j) g[j] = ((uint32_t)b[2 * j] << 8) | b[2 * j + 1];
+                int zs = 255, ze = 255;   // the first longest run of >= 2 zero groups
+                for (int s = 0; s < 8; ++s) {
+                    int e = s;
+                    while (e < 8 && g[e] == 0) ++e;
+                    if (e - s >= 2 && e - s > ze - zs) { zs = s; ze = e; }
+                }
+                for (int s = 0; s < 8; ++s) {
+                    if (s == zs) {
+                        o[p++] = ':';
+                        o[p++] = ':';
+                        s = ze;
+                        if (s >= 8) break;
+                    } else if (s > 0) {
+                        o[p++] = ':';
+                    }
+                    p = ip_put_hex(o, p, g[s]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // write the block's rows x IPW bytes out as 8-B stores
+    const uint64_t row0 = (uint64_t)blockIdx.x * TB;
+    const uint64_t rows = n - row0 < (uint64_t)TB ? n - row0 : (uint64_t)TB;
+    uint2 *dst = reinterpret_cast<uint2 *>(out + row0 * IPW);
+    for (uint32_t q = threadIdx.x; q < rows * (IPW / 8); q += TB) dst[q] = buf[q / (IPW / 8)][q % (IPW / 8)];
+}
+
 }  // namespace
+
+int launch_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t astride, const uint8_t *fam, uint32_t fstride,
+                   const uint32_t *rowmap, uint64_t n, uint8_t *out) {
+    if (n == 0) return IGX_OK;
+    hipLaunchKernelGGL(k_ip_text, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, ctx->stream, addr, astride, fam,
+                       fstride, rowmap, n, out);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
 
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
@@ -468,6 +567,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         ca.desc[k] = keys[k].desc_eff;
         ca.words[k] = keys[k].words;
         ca.rstride[k] = keys[k].stride ? keys[k].stride : keys[k].width;
+        ca.direct[k] = keys[k].direct;
         KW += keys[k].words;
     }
     ca.rowmap = rowmap;

@@ -190,6 +190,9 @@ class Table:
             if src == _abi.TSRC_KEY:
                 off, w, kind = what
                 ts.append(_abi.TSortKey(src, 0, off, w, kind, int(desc)))
+            elif src == _abi.TSRC_IPTEXT:
+                addr_off, fam_off = what
+                ts.append(_abi.TSortKey(src, fam_off, addr_off, 16, _abi.KIND_BYTES, int(desc)))
             else:
                 ts.append(_abi.TSortKey(src, int(what or 0), 0, 0, 0, int(desc)))
         arr = (_abi.TSortKey * max(1, len(ts)))(*ts)
@@ -284,6 +287,23 @@ def partition_rows(rows, key_bytes, nparts):
     cnt = torch.zeros(nparts, dtype=torch.int64, device=rows.device)
     ctx.check(ctx.L.igx_partition_rows(ctx.h, ptr(rows), n, rb, key_bytes, nparts, ptr(out), ptr(cnt)))
     return out, cnt.cpu().tolist()
+
+
+def ip_text(addr, family, n=None, rowmap=None):
+    """igx_ip_text: IPStringFromBytes (helpers.go:111-120) of n rows on the device.
+    addr: uint8 (n, 16) or a byte view with a row stride; family: u16 column (or a byte view
+    whose first two bytes per row are the family).  Returns uint8 (n, IPTEXT_WIDTH),
+    zero-padded texts."""
+    torch = torch_mod()
+    ctx = context()
+    n = addr.shape[0] if n is None else n
+    astride = addr.stride(0) * addr.element_size()
+    fstride = family.stride(0) * family.element_size()
+    out = torch.empty((max(1, n), _abi.IPTEXT_WIDTH), dtype=torch.uint8, device=addr.device)
+    if n:
+        ctx.check(ctx.L.igx_ip_text(ctx.h, ptr(addr), astride, ptr(family), fstride,
+                                    None if rowmap is None else ptr(rowmap), n, ptr(out)))
+    return out[:n]
 
 
 def ingest_aos(records, n, rec_bytes, fields, device=None):

@@ -159,6 +159,8 @@ class _TopTracer:
             desc = bool(sk.desc)
             if src[0] == "agg":
                 keys.append((_abi.TSRC_AGG, src[1], desc))
+            elif src[0] == "iptext":      # Saddr / Daddr: IPStringFromBytes text order
+                keys.append((_abi.TSRC_IPTEXT, (self.key_off[src[1]], self.key_off[src[2]]), desc))
             elif src[0] == "key":
                 f = src[1]
                 kind = src[2] if len(src) > 2 else sk.kind
@@ -277,7 +279,8 @@ class TopTcpTracer(_TopTracer):
                                 extractors=("ip", "sent", "recv"), virtual=("local", "remote"))
     SORT_SRC = dict(_ENRICH, mntns=("key", "mntns"), pid=("key", "pid", _abi.KIND_INT),
                     comm=("key", "comm"), ip=("key", "family"), sport=("key", "lport"),
-                    dport=("key", "dport"), sent=("agg", 0), recv=("agg", 1))
+                    dport=("key", "dport"), sent=("agg", 0), recv=("agg", 1),
+                    saddr=("iptext", "saddr", "family"), daddr=("iptext", "daddr", "family"))
     SortByDefault = ["-sent", "-recv"]      # types.go:27
 
     def __init__(self, TargetPid=0, TargetFamily=-1, **kw):

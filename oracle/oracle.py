@@ -623,6 +623,54 @@ def top_tcp(ev, k=20, base_idx=0, max_groups=None):
     return G, keys[:m], sent[:m], recv[:m], first[:m]
 
 
+def ip_string(b16, family: int) -> str:
+    """gadgets.IPStringFromBytes (pkg/gadgets/helpers.go:111-120) with ipType chosen as the
+    tcp tracer does (top/tcp/tracer/tracer.go:199-206: 6 iff family == AF_INET6), restating
+    Go's net/netip Addr.String: string4 dotted decimal; Is4In6 -> "::ffff:" + string4 of the
+    last four bytes; else appendTo6 -- lowercase hex groups without leading zeros, the first
+    longest run of >= 2 zero groups replaced by "::"."""
+    b = bytes(b16)
+    if family != 10:
+        return ".".join(str(x) for x in b[:4])
+    if b[:10] == bytes(10) and b[10:12] == b"\xff\xff":
+        return "::ffff:" + ".".join(str(x) for x in b[12:16])
+    g = [(b[2 * i] << 8) | b[2 * i + 1] for i in range(8)]
+    zs, ze = 255, 255
+    for i in range(8):
+        j = i
+        while j < 8 and g[j] == 0:
+            j += 1
+        if j - i >= 2 and j - i > ze - zs:
+            zs, ze = i, j
+    out = []
+    i = 0
+    while i < 8:
+        if i == zs:
+            out.append("::")
+            i = ze
+            if i >= 8:
+                break
+        elif i > 0:
+            out.append(":")
+        out.append("%x" % g[i])
+        i += 1
+    return "".join(out)
+
+
+def ip_text_rows(addr, family, width=40):
+    """(n, width) zero-padded ip_string texts (the device layout of igx_ip_text)."""
+    n = addr.shape[0]
+    out = np.zeros((n, width), np.uint8)
+    memo = {}
+    for i in range(n):
+        key = (addr[i].tobytes(), int(family[i]))
+        t = memo.get(key)
+        if t is None:
+            t = memo[key] = ip_string(key[0], key[1]).encode()
+        out[i, :len(t)] = np.frombuffer(t, np.uint8)
+    return out
+
+
 # ------------------------------------------------------------------------------------
 # GroupEntries (pkg/columns/group/group.go:27-165) on Python row objects
 # ------------------------------------------------------------------------------------

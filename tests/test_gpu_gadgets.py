@@ -118,6 +118,84 @@ def test_top_tcp_sort_by_key_columns(oracle, igx, torch, G):
         tr.destroy()
 
 
+def _ip_cases():
+    """Edge cases of netip's text form: all-zero, loopback, leading / trailing / tied zero
+    runs, a single zero group (never "::"), IPv4-mapped, and family != AF_INET6."""
+    v6 = ["::", "::1", "1::", "1:0:1::1:0:0", "2001:db8::1", "2001:db8:0:1:0:0:0:1", "fe80::1:2:3:4",
+          "ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff", "0:1:0:1:0:1:0:1", "1:2:3:4:5:6:7:0", "::ffff:10.0.0.1",
+          "::ffff:0:0", "::fffe:1.2.3.4", "abcd:ef01::"]
+    import ipaddress
+    rows = [(ipaddress.IPv6Address(a).packed, 10) for a in v6]
+    rows += [(bytes([10, 0, 255, 7]) + bytes(12), 2), (bytes([0, 0, 0, 0]) + bytes(range(12)), 2),
+             (bytes([192, 168, 1, 100]) + bytes(12), 0), (bytes(range(16)), 7)]
+    return rows
+
+
+def test_ip_text_matches_netip(oracle, igx, torch):
+    """igx_ip_text == IPStringFromBytes (helpers.go:111-120) on edge cases and random
+    addresses, through a row map."""
+    H = igx.columns
+    rng = np.random.default_rng(11)
+    rows = _ip_cases()
+    for _ in range(5000):
+        g = rng.integers(0, 3, 8)
+        v = rng.integers(0, 65536, 8) * (g > 0)
+        rows.append((b"".join(int(x).to_bytes(2, "big") for x in v), int(rng.choice([2, 10, 10]))))
+    n = len(rows)
+    addr = np.frombuffer(b"".join(r[0] for r in rows), np.uint8).reshape(n, 16).copy()
+    fam = np.array([r[1] for r in rows], np.uint16)
+    want = oracle.ip_text_rows(addr, fam)
+    got = H.host(igx.engine.ip_text(H.to_device(addr), H.to_device(fam)))
+    assert np.array_equal(got, want)
+    for i in range(len(_ip_cases())):
+        assert bytes(got[i]).rstrip(b"\0").decode() == G_ipstr(igx, rows[i])
+    rowmap = rng.permutation(n).astype(np.int32)
+    got2 = H.host(igx.engine.ip_text(H.to_device(addr), H.to_device(fam), rowmap=H.to_device(rowmap)))
+    assert np.array_equal(got2, want[rowmap])
+
+
+def G_ipstr(igx, row):
+    return igx.gadgets.IPStringFromBytes(row[0], 6 if row[1] == 10 else 4)
+
+
+def test_top_tcp_sort_by_addresses(oracle, igx, torch, G):
+    """SortBy saddr / daddr: the Stats strings (tracer.go:199-206) in Go string order."""
+    H = igx.columns
+    Gk, n = 3000, 100_000
+    ev_h = oracle.gen_tcp(0xC2, 2, Gk, oracle.zipf_cdf(Gk, 1.1), 0, n)
+    rng = np.random.default_rng(3)
+    pool = np.frombuffer(b"".join(a for a, _ in _ip_cases()[:14]), np.uint8).reshape(14, 16)
+    sel = rng.random(n) < 0.3
+    ev_h["family"][sel] = 10
+    ev_h["saddr"][sel] = pool[rng.integers(0, 14, int(sel.sum()))]
+    ev_h["daddr"][sel] = pool[rng.integers(0, 14, int(sel.sum()))]
+    ev = _dev(H, ev_h)
+    names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family")
+
+    def text(off):
+        return lambda g: oracle.ip_text_rows(g["keys"][:, off:off + 16],
+                                             g["keys"][:, 68:70].copy().view(np.uint16).ravel())
+    for sort_by in (["saddr"], ["-daddr", "recv"], ["-saddr", "-daddr"], ["daddr", "-sent"]):
+        tr = G.TopTcpTracer(SortBy=sort_by, capacity=1 << 17)
+        tr.feed(ev)
+        stats = tr.nextStats()
+        spec = []
+        for s_ in sort_by:
+            d, c = s_.startswith("-"), s_.lstrip("-")
+            spec.append({"saddr": (text(0), "string", d), "daddr": (text(16), "string", d),
+                         "recv": (_agg_col(1), "uint64", d), "sent": (_agg_col(0), "uint64", d)}[c])
+        Gn, _, _, first = _ref_top(
+            oracle, {k: ev_h[k] for k in names},
+            [{"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 0},
+             {"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 1}],
+            (ev_h["family"] == 2) | (ev_h["family"] == 10), spec, n)
+        assert [s.FirstIndex for s in stats] == [int(x) for x in first], sort_by
+        # and the strings the rows carry are in that order
+        key = [s.Saddr if sort_by[0].lstrip("-") == "saddr" else s.Daddr for s in stats]
+        assert key == sorted(key, key=lambda x: x.encode(), reverse=sort_by[0].startswith("-"))
+        tr.destroy()
+
+
 def _file_events(n, G_keys, seed=5):
     rng = np.random.default_rng(seed)
     kid = rng.zipf(1.3, n) % G_keys
