@@ -309,6 +309,29 @@ int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32
  * tcptopTrafficT, pkg/gadgets/top/tcp/tracer/tcptop_bpfel_x86.go:15-30) are cut into SoA
  * columns: field f (byte offset field_off[f], field_width[f] bytes) of record r goes to
  * out_cols[f] + r * field_width[f].  1..16 fields.  Async. */
+/* trace open's perf-ring samples (struct event, pkg/gadgets/trace/open/tracer/bpf/opensnoop.h:14-24,
+ * bpf2go opensnoopEvent: ts u64 @0, pid u32 @8, uid u32 @12, mntns u64 @16, ret s32 @24,
+ * flags s32 @28, comm[16] @32, fname[255] @48; 304 bytes) -> the Event fields the tracer's
+ * run loop fills (trace/open/tracer/tracer.go:182-208):
+ *   timestamp = WallTimeFromBootTime(ts) = ts + boot_to_wall_ns;  ret = int(Ret) (sign-
+ *   extended); fd = ret >= 0 ? ret : 0;  err = ret < 0 ? -ret : 0;  comm / path =
+ *   FromCString (the bytes before the first NUL; the rest of the row zeroed; path rows are
+ *   256 bytes, the 255-byte name plus a NUL).
+ * samples: device, n x sample_bytes (sample_bytes >= 304, a multiple of 8; 8-byte aligned).
+ * Null output columns are skipped.  Asynchronous. */
+typedef struct {
+    int64_t *timestamp;
+    uint32_t *pid;
+    uint32_t *uid;
+    uint64_t *mntns;
+    int64_t *ret;
+    int64_t *fd;
+    int64_t *err;
+    uint8_t *comm;   /* n x 16 */
+    uint8_t *path;   /* n x 256 */
+} igx_open_cols;
+int igx_ingest_open_events(igx_ctx *ctx, const uint8_t *samples, uint64_t n, uint32_t sample_bytes,
+                           int64_t boot_to_wall_ns, const igx_open_cols *out);
 int igx_ingest_aos(igx_ctx *ctx, const void *records, uint64_t nrec, uint32_t rec_bytes,
                    const uint32_t *field_off, const uint32_t *field_width, uint32_t nfields,
                    void *const *out_cols);

@@ -66,6 +66,15 @@ class TSortKey(C.Structure):
                 ("width", C.c_uint32), ("kind", C.c_uint32), ("desc", C.c_uint32)]
 
 
+class OpenCols(C.Structure):
+    """igx_open_cols: device outputs of igx_ingest_open_events (NULL = skipped)."""
+    _fields_ = [(f, C.c_void_p) for f in ("timestamp", "pid", "uid", "mntns", "ret", "fd", "err",
+                                           "comm", "path")]
+
+
+OPEN_SAMPLE_BYTES = 304
+
+
 class IgxError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"igx error {code}: {msg}")
@@ -112,6 +121,7 @@ SIGNATURES = [
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
     ("igx_partition_rows", _I, [_VP, _VP, _U64, _U32, _U32, _U32, _VP, _VP]),
+    ("igx_ingest_open_events", _I, [_VP, _VP, _U64, _U32, C.c_int64, C.POINTER(OpenCols)]),
     ("igx_ingest_aos", _I, [_VP, _VP, _U64, _U32, C.POINTER(_U32), C.POINTER(_U32), _U32,
                             C.POINTER(_VP)]),
     ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),

@@ -183,6 +183,71 @@ extern "C" int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nr
     return IGX_OK;
 }
 
+// ---- trace open perf samples -> Event columns (one wave per sample) --------------------------
+namespace {
+constexpr uint32_t OPEN_SAMPLE = 304;   // sizeof(struct event), 8-byte aligned
+
+// FromCString over a row held as one dword per lane (lanes [0, nl)): keeps the bytes before the
+// first NUL (bytes at index >= lim count as NUL), zeroes the rest
+__device__ __forceinline__ uint32_t cstring_cut(uint32_t v, uint32_t lane, uint32_t nl, uint32_t lim) {
+    uint32_t first = 4;   // first NUL byte in this lane's dword (4 = none)
+    for (int j = 3; j >= 0; --j) {
+        const bool nul = ((v >> (8 * j)) & 0xFFu) == 0 || 4 * lane + j >= lim;
+        if (nul) first = (uint32_t)j;
+    }
+    const uint64_t m = __ballot(lane < nl && first < 4);
+    const uint32_t L = m ? (uint32_t)__ffsll((long long)m) - 1 : 64u;
+    if (lane > L) return 0;
+    if (lane == L) return first == 0 ? 0u : (v & (0xFFFFFFFFu >> (32 - 8 * first)));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_ingest_open(const uint8_t *__restrict__ s, uint64_t n, uint32_t sb,
+                                                     int64_t boot, igx_open_cols o) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wpb = 256 / 64;
+    for (uint64_t r = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6); r < n; r += (uint64_t)gridDim.x * wpb) {
+        const uint8_t *rec = s + r * sb;
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(rec);
+        // fname: bytes 48..303 = dword 12 + lane; byte 255 of the row is the struct's padding
+        const uint32_t f = __builtin_nontemporal_load(d + 12 + lane);
+        const uint32_t pf = cstring_cut(f, lane, 64, 255);
+        if (o.path) reinterpret_cast<uint32_t *>(o.path + r * 256)[lane] = pf;
+        const uint32_t c = lane < 4 ? d[8 + lane] : 0u;
+        const uint32_t pc = cstring_cut(c, lane, 4, 16);
+        if (o.comm && lane < 4) reinterpret_cast<uint32_t *>(o.comm + r * 16)[lane] = pc;
+        if (lane == 0) {
+            const uint64_t ts = *reinterpret_cast<const uint64_t *>(rec);
+            const int64_t ret = (int64_t) * reinterpret_cast<const int32_t *>(rec + 24);
+            if (o.timestamp) o.timestamp[r] = (int64_t)(ts + (uint64_t)boot);
+            if (o.pid) o.pid[r] = d[2];
+            if (o.uid) o.uid[r] = d[3];
+            if (o.mntns) o.mntns[r] = *reinterpret_cast<const uint64_t *>(rec + 16);
+            if (o.ret) o.ret[r] = ret;
+            if (o.fd) o.fd[r] = ret >= 0 ? ret : 0;
+            if (o.err) o.err[r] = ret < 0 ? -ret : 0;
+        }
+    }
+}
+}  // namespace
+
+extern "C" int igx_ingest_open_events(igx_ctx *ctx, const uint8_t *samples, uint64_t n, uint32_t sample_bytes,
+                                      int64_t boot_to_wall_ns, const igx_open_cols *out) {
+    if (!ctx) return IGX_EINVAL;
+    if (!out) return igx_fail(ctx, IGX_EINVAL, "ingest_open: null output");
+    if (n == 0) return IGX_OK;
+    if (!samples) return igx_fail(ctx, IGX_EINVAL, "ingest_open: null samples");
+    if (sample_bytes < OPEN_SAMPLE || sample_bytes % 8 || reinterpret_cast<uintptr_t>(samples) % 8)
+        return igx_fail(ctx, IGX_EINVAL, "ingest_open: samples must be >= %u bytes, 8-byte aligned", OPEN_SAMPLE);
+    if ((out->path && reinterpret_cast<uintptr_t>(out->path) % 4) || (out->comm && reinterpret_cast<uintptr_t>(out->comm) % 4))
+        return igx_fail(ctx, IGX_EINVAL, "ingest_open: comm / path columns must be 4-byte aligned");
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((uint64_t)ctx->num_cus * 8, (n + 3) / 4);
+    hipLaunchKernelGGL(k_ingest_open, dim3(blocks), dim3(256), 0, ctx->stream, samples, n, sample_bytes,
+                       boot_to_wall_ns, *out);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
+
 extern "C" int igx_ingest_aos(igx_ctx *ctx, const void *records, uint64_t nrec, uint32_t rec_bytes,
                               const uint32_t *field_off, const uint32_t *field_width, uint32_t nfields,
                               void *const *out_cols) {

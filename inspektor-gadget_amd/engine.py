@@ -306,6 +306,29 @@ def ip_text(addr, family, n=None, rowmap=None):
     return out[:n]
 
 
+def ingest_open_events(samples, n=None, sample_bytes=_abi.OPEN_SAMPLE_BYTES, boot_to_wall_ns=0):
+    """igx_ingest_open_events: trace open perf samples (device uint8, n x sample_bytes) ->
+    the Event columns of trace/open/tracer/tracer.go:182-208 (timestamp, pid, uid, mntns, ret,
+    fd, err as int64 / u32 / u64 tensors; comm (n, 16) and path (n, 256) uint8)."""
+    torch = torch_mod()
+    ctx = context()
+    n = samples.numel() // sample_bytes if n is None else n
+    dev = samples.device
+    m = max(1, n)
+    cols = {"timestamp": torch.empty(m, dtype=torch.int64, device=dev),
+            "pid": torch.empty(m, dtype=torch.uint32, device=dev),
+            "uid": torch.empty(m, dtype=torch.uint32, device=dev),
+            "mntns": torch.empty(m, dtype=torch.uint64, device=dev),
+            "ret": torch.empty(m, dtype=torch.int64, device=dev),
+            "fd": torch.empty(m, dtype=torch.int64, device=dev),
+            "err": torch.empty(m, dtype=torch.int64, device=dev),
+            "comm": torch.empty((m, 16), dtype=torch.uint8, device=dev),
+            "path": torch.empty((m, 256), dtype=torch.uint8, device=dev)}
+    oc = _abi.OpenCols(*[cols[f].data_ptr() for f, _ in _abi.OpenCols._fields_])
+    ctx.check(ctx.L.igx_ingest_open_events(ctx.h, ptr(samples), n, sample_bytes, boot_to_wall_ns, C.byref(oc)))
+    return {k: v[:n] for k, v in cols.items()}
+
+
 def ingest_aos(records, n, rec_bytes, fields, device=None):
     """igx_ingest_aos: records (device uint8, n x rec_bytes) -> {name: SoA column}.
     fields: [(name, offset, width, dtype)] with dtype a torch dtype (width 1/2/4/8) or

@@ -623,6 +623,32 @@ def top_tcp(ev, k=20, base_idx=0, max_groups=None):
     return G, keys[:m], sent[:m], recv[:m], first[:m]
 
 
+def from_cstring_rows(a, width):
+    """gadgets.FromCString per row (bytes before the first NUL), zero-padded to width."""
+    n, w = a.shape
+    out = np.zeros((n, width), np.uint8)
+    nul = (a == 0)
+    first = np.where(nul.any(axis=1), nul.argmax(axis=1), w)
+    keep = np.arange(w)[None, :] < first[:, None]
+    out[:, :w] = np.where(keep, a, 0)
+    return out
+
+
+def decode_open_events(samples, boot_to_wall_ns=0):
+    """trace/open/tracer/tracer.go:182-208 over raw perf samples (n, >=304) of struct event
+    (opensnoop.h:14-24; bpf2go opensnoopEvent offsets ts 0, pid 8, uid 12, mntns 16, ret 24,
+    flags 28, comm 32, fname 48..302)."""
+    s = np.ascontiguousarray(samples)
+    n = s.shape[0]
+    u64 = lambda off: s[:, off:off + 8].copy().view(np.uint64).ravel()   # noqa: E731
+    u32 = lambda off: s[:, off:off + 4].copy().view(np.uint32).ravel()   # noqa: E731
+    ret = s[:, 24:28].copy().view(np.int32).ravel().astype(np.int64)
+    return {"timestamp": (u64(0) + np.uint64(boot_to_wall_ns & 0xFFFFFFFFFFFFFFFF)).view(np.int64),
+            "pid": u32(8), "uid": u32(12), "mntns": u64(16), "ret": ret,
+            "fd": np.where(ret >= 0, ret, 0), "err": np.where(ret < 0, -ret, 0),
+            "comm": from_cstring_rows(s[:, 32:48], 16), "path": from_cstring_rows(s[:, 48:303], 256)}
+
+
 def ip_string(b16, family: int) -> str:
     """gadgets.IPStringFromBytes (pkg/gadgets/helpers.go:111-120) with ipType chosen as the
     tcp tracer does (top/tcp/tracer/tracer.go:199-206: 6 iff family == AF_INET6), restating

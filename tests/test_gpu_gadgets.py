@@ -340,3 +340,66 @@ def test_parser_pipeline_c1(oracle, igx, torch):
     got.clear()
     p.Flush()
     assert got[0].n == 2 * len(sel)
+
+
+def _open_samples(n, seed=21):
+    """Raw opensnoop perf samples: random garbage after each C string's NUL, names with no
+    NUL at all (255 bytes), comm with no NUL (16 bytes), negative rets, random padding."""
+    rng = np.random.default_rng(seed)
+    s = rng.integers(0, 256, (n, 304), dtype=np.uint8)
+    s[:, 8:12] = rng.integers(0, 40000, n).astype(np.uint32).view(np.uint8).reshape(n, 4)
+    s[:, 24:28] = np.where(rng.random(n) < 0.1, rng.integers(-13, 0, n), rng.integers(3, 1024, n)).astype(
+        np.int32).view(np.uint8).reshape(n, 4)
+    names = [b"bash", b"sshd", b"containerd", b"kubelet", b"node_exporter", b"x" * 16]
+    for i in range(n):
+        nm = names[i % len(names)]
+        s[i, 32:32 + len(nm)] = np.frombuffer(nm, np.uint8)
+        if len(nm) < 16:
+            s[i, 32 + len(nm)] = 0
+        k = int(rng.integers(0, 256))
+        if k < 255:
+            s[i, 48 + k] = 0          # else: no NUL in the 255 name bytes
+        s[i, 48:48 + min(k, 3)] = np.frombuffer(b"/et"[:min(k, 3)], np.uint8)
+    return s
+
+
+def test_trace_open_samples_decode(oracle, igx, torch):
+    """igx_ingest_open_events == tracer.go:182-208 over raw struct event samples."""
+    H = igx.columns
+    n = 20_001
+    s = _open_samples(n)
+    boot = 1_700_000_000_123_456_789
+    got = igx.engine.ingest_open_events(H.to_device(s), boot_to_wall_ns=boot)
+    want = oracle.decode_open_events(s, boot)
+    for k, v in want.items():
+        g = H.host(got[k])
+        assert np.array_equal(g.view(v.dtype) if g.dtype != v.dtype else g, v), k
+    # a stride larger than the struct (samples with trailing bytes)
+    s2 = np.concatenate([s[:777], np.zeros((777, 16), np.uint8)], axis=1)
+    got2 = igx.engine.ingest_open_events(H.to_device(s2), sample_bytes=320)
+    assert np.array_equal(H.host(got2["path"]), want["path"][:777])
+
+
+def test_trace_open_pipeline_from_samples(oracle, igx, torch):
+    """C1 from the wire: perf samples -> Event columns -> filters ["err:0","pid:>=1000"] ->
+    sort ["comm","-pid"] (parser.go:199-224), against the oracle's decode + Go sort."""
+    import importlib
+    P = importlib.import_module("inspektor-gadget_amd.parser")
+    H = igx.columns
+    n = 30_000
+    s = _open_samples(n, seed=5)
+    batch = igx.wire.trace_open_batch(H.to_device(s))
+    p = P.NewParser(batch.cols)
+    p.SetFilters(["err:0", "pid:>=1000", "path:~^/et"])
+    p.SetSorting(["comm", "-pid"])
+    got = []
+    p.SetEventCallback(got.append)
+    p.EventHandlerFuncArray()(batch)
+    ev = oracle.decode_open_events(s)
+    sel = np.nonzero((ev["err"] == 0) & (ev["pid"] >= 1000) &
+                     (ev["path"][:, 0] == ord("/")) & (ev["path"][:, 1] == ord("e")) & (ev["path"][:, 2] == ord("t")))[0]
+    perm = oracle.go_sort_entries([(ev["comm"][sel], "string", False), (ev["pid"][sel], "uint32", True)], len(sel))
+    out = got[0]
+    assert out.n == len(sel) > 0
+    assert np.array_equal(H.host(out["pid"]), ev["pid"][sel][perm])
+    assert np.array_equal(H.host(out["path"]), ev["path"][sel][perm])
