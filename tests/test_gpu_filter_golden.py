@@ -1,0 +1,71 @@
+"""The reference's filter table (pkg/columns/filter/filter_test.go:50-298, re-encoded in
+tests/golden/filter_table.json) run through the device scan: every row's filter is parsed
+by igx_filter_parse and evaluated by igx_filter (k_filter.hip) over the 5 records + nil held
+as device columns; the selected count must equal the table's.  Regex rows take the device
+DFA, float rows the IEEE compares, the int8:300 row the Convert truncation."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+NP = {"int": np.int64, "int8": np.int8, "int16": np.int16, "int32": np.int32, "int64": np.int64,
+      "uint": np.uint64, "uint8": np.uint8, "uint16": np.uint16, "uint32": np.uint32, "uint64": np.uint64,
+      "float32": np.float32, "float64": np.float64}
+
+
+def _device_fixture(igx):
+    H = igx.columns
+    d = json.load(open(os.path.join(GOLDEN, "filter_table.json")))
+    recs = d["records"]
+    n = len(recs)
+    schema, data = [], {}
+    for name, kind in d["columns"]:
+        if kind == "string":
+            schema.append((name, "string", 16))
+            a = np.zeros((n, 16), np.uint8)
+            for i, r in enumerate(recs):
+                if r is not None:
+                    b = r["string"].encode()
+                    a[i, :len(b)] = np.frombuffer(b, np.uint8)
+        elif kind in NP:
+            schema.append((name, kind))
+            a = np.zeros(n, NP[kind])
+            for i, r in enumerate(recs):
+                if r is not None and name != "time":
+                    a[i] = r["v"]
+        else:
+            schema.append((name, kind))
+            a = np.zeros(n, np.uint8)
+        data[name] = H.to_device(a)
+    valid = H.to_device(np.array([r is not None for r in recs], np.uint8))
+    cols = H.Columns(schema)
+    return d, cols, H.EventBatch(cols, data, valid=valid)
+
+
+def test_filter_table_on_device(igx):
+    F, H = igx.filter, igx.columns
+    d, cols, batch = _device_fixture(igx)
+    assert len(d["rows"]) == 111
+    ran = 0
+    for row in d["rows"]:
+        try:
+            spec = F.GetFilterFromString(cols, row["filter"])
+        except F.FilterError:
+            assert row["error"], row
+            continue
+        assert not row["error"], row
+        got = H.host(F.FilterSpecs([spec]).MatchAll(batch)) if hasattr(F, "FilterSpecs") else \
+            H.host(F.GetFiltersFromStrings(cols, [row["filter"]]).MatchAll(batch))
+        assert len(got) == row["count"], row
+        ran += 1
+    assert ran == sum(not r["error"] for r in d["rows"]) == 84
+
+
+def test_filter_table_multi_on_device(igx):
+    F, H = igx.filter, igx.columns
+    d, cols, batch = _device_fixture(igx)
+    sel = H.host(F.GetFiltersFromStrings(cols, d["multi"]["filters"]).MatchAll(batch))
+    assert len(sel) == 1
