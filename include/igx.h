@@ -283,6 +283,16 @@ int igx_np_mark(igx_ctx *ctx, const uint8_t *typ, const uint8_t *pkt, const uint
  * ndev == 0 is the shipped gadget's keying (no targ_per_disk / targ_per_flag): every row
  * is device index 0 and dev may be NULL.  cont may be NULL (ncont must then be 1).
  * hist (device u32, max(ndev,1)*ncont*nslots) accumulates.  Async. */
+/* GroupEntries' float group:sum (group.go:133-156, flattenValues): perm (device u32, n) is a
+ * stable sort of the rows by the group key (key_bytes at row * key_stride of keys); each run
+ * of equal keys is one group in input order.  For each run, out[first row of the run] =
+ * v[first] + v[second] + ... in that order, in float64, rounded to float32 after every add
+ * when val_width is 4 (SetFloat on a float32 field).  Rows with valid[row] == 0 (nullable)
+ * are nil entries and belong to no run.  Other out entries are left untouched.  Async. */
+int igx_segment_fsum(igx_ctx *ctx, const uint8_t *keys, uint32_t key_stride, uint32_t key_bytes,
+                     const uint32_t *perm, uint64_t n, const uint8_t *valid, const void *vals,
+                     uint32_t val_width, double *out);
+
 /* IPStringFromBytes (pkg/gadgets/helpers.go:111-120) for n rows: addr (16 bytes at row *
  * addr_stride) rendered as netip.AddrFrom16(...).String() when the u16 family at row *
  * family_stride is AF_INET6 (10), else netip.AddrFrom4(addr[0:4]).String().  out (device,

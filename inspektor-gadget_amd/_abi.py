@@ -113,6 +113,7 @@ SIGNATURES = [
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
     ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
+    ("igx_segment_fsum", _I, [_VP, _VP, _U32, _U32, _VP, _U64, _VP, _VP, _U32, _VP]),
     ("igx_ip_text", _I, [_VP, _VP, _U32, _VP, _U32, _VP, _U64, _VP]),
     ("igx_groupby_reset", _I, [_VP]),
     ("igx_groupby_destroy", _I, [_VP]),

@@ -541,7 +541,60 @@ __global__ __launch_bounds__(TB) void k_ip_text(const uint8_t *__restrict__ addr
     for (uint32_t q = threadIdx.x; q < rows * (IPW / 8); q += TB) dst[q] = buf[q / (IPW / 8)][q % (IPW / 8)];
 }
 
+// ---- GroupEntries' float group:sum (pkg/columns/group/group.go:133-156) ---------------------
+// flattenValues starts from the group's first entry and, for every later entry in input
+// order, does field = SetFloat(field.Float() + cur.Float()): float64 addition, then the
+// field's own rounding (a float32 column rounds after every add).  That order is kept: perm is
+// a stable sort of the rows by the group key, so each group is one contiguous run in input
+// order; the thread at a run's first row walks the run.
+__global__ __launch_bounds__(TB) void k_segment_fsum(const uint8_t *__restrict__ keys, uint32_t kstride,
+                                                     uint32_t kbytes, const uint32_t *__restrict__ perm,
+                                                     uint64_t n, const uint8_t *__restrict__ valid,
+                                                     const uint8_t *__restrict__ vals, uint32_t vwidth,
+                                                     double *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = perm[i];
+    if (valid && !valid[r]) return;
+    auto same = [&](uint32_t a, uint32_t b) {
+        const uint8_t *p = keys + (uint64_t)a * kstride, *q = keys + (uint64_t)b * kstride;
+        for (uint32_t j = 0; j < kbytes; ++j)
+            if (p[j] != q[j]) return false;
+        return true;
+    };
+    if (i > 0) {
+        const uint32_t pr = perm[i - 1];
+        if ((!valid || valid[pr]) && same(pr, r)) return;   // not the first row of its run
+    }
+    auto val = [&](uint32_t row) -> double {
+        return vwidth == 4 ? (double)reinterpret_cast<const float *>(vals)[row]
+                           : reinterpret_cast<const double *>(vals)[row];
+    };
+    double s = val(r);
+    for (uint64_t j = i + 1; j < n; ++j) {
+        const uint32_t q = perm[j];
+        if ((valid && !valid[q]) || !same(q, r)) break;
+        s = s + val(q);
+        if (vwidth == 4) s = (double)(float)s;   // SetFloat on a float32 field
+    }
+    out[r] = s;
+}
+
 }  // namespace
+
+extern "C" int igx_segment_fsum(igx_ctx *ctx, const uint8_t *keys, uint32_t key_stride, uint32_t key_bytes,
+                                const uint32_t *perm, uint64_t n, const uint8_t *valid, const void *vals,
+                                uint32_t val_width, double *out) {
+    if (!ctx) return IGX_EINVAL;
+    if (n == 0) return IGX_OK;
+    if (!keys || !perm || !vals || !out) return igx_fail(ctx, IGX_EINVAL, "segment_fsum: null argument");
+    if (val_width != 4 && val_width != 8) return igx_fail(ctx, IGX_EINVAL, "segment_fsum: float width %u", val_width);
+    if (n >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "segment_fsum: too many rows");
+    hipLaunchKernelGGL(k_segment_fsum, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, ctx->stream, keys,
+                       key_stride, key_bytes, perm, n, valid, static_cast<const uint8_t *>(vals), val_width, out);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
 
 int launch_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t astride, const uint8_t *fam, uint32_t fstride,
                    const uint32_t *rowmap, uint64_t n, uint8_t *out) {

@@ -238,9 +238,11 @@ def table_tensors(tab, fin):
     rows = tab.gather(slots)
     kb = fin["key_bytes"]
     keys = rows[:, :kb].contiguous()
-    aggs = [rows[:, kb + 8 * i: kb + 8 * i + 8].contiguous().view(torch.uint64).flatten()
+    # flat copies: a one-row slice counts as contiguous and keeps its byte offset and row
+    # stride, which a u64 view rejects
+    aggs = [rows[:, kb + 8 * i: kb + 8 * i + 8].reshape(-1).clone().view(torch.uint64)
             for i in range(tab.naggs)]
-    first = rows[:, kb + 8 * tab.naggs:].contiguous().view(torch.uint64).flatten()
+    first = rows[:, kb + 8 * tab.naggs:].reshape(-1).clone().view(torch.uint64)
     return keys, aggs, first
 
 

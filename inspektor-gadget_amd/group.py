@@ -7,8 +7,12 @@ group_test.go:101-129); each output row is a copy of the group's first row with 
 sorted ascending by the group column (:115).  "" groups everything into one row and stops.
 
 Device path: igx_groupby (exact keys, first-occurrence index) -> gather first rows ->
-overwrite sums -> igx_sort_perm.  Float `group:sum` columns would need the reference's
-sequential float64 addition order and are rejected (IGX_ENOTSUP).
+overwrite sums -> igx_sort_perm.  Float `group:sum` columns keep the reference's sequential
+addition order (float64 adds, a float32 field rounding after each): a stable sort of the rows
+by the group key makes each group one run in input order, and igx_segment_fsum walks the
+runs.  Groups are keyed by the column's bytes; the reference keys by the value's string form
+(getStringFromValue, :27-47), which differs only for floats whose distinct bit patterns print
+alike (NaN payloads).
 """
 from __future__ import annotations
 
@@ -39,10 +43,9 @@ def _group_one(cols: Columns, batch: EventBatch, col, all_rows: bool):
     torch = torch_mod()
     dev = batch.device()
     n = batch.n
-    sums = [c for c in cols.GetOrderedColumns() if c.GroupType == GroupTypeSum and not c.virtual]
-    for c in sums:
-        if KINDS[c.kind][0] == _abi.KIND_FLOAT:
-            raise IgxError(_abi.IGX_ENOTSUP, f"float group:sum column {c.Name!r} on the GPU path")
+    every = [c for c in cols.GetOrderedColumns() if c.GroupType == GroupTypeSum and not c.virtual]
+    sums = [c for c in every if KINDS[c.kind][0] != _abi.KIND_FLOAT]
+    fsums = [c for c in every if KINDS[c.kind][0] == _abi.KIND_FLOAT]
     tensors = batch.tensors_in_schema_order()
     if all_rows:
         keycol = torch.zeros(max(1, n), dtype=torch.uint32, device=dev)
@@ -76,9 +79,22 @@ def _group_one(cols: Columns, batch: EventBatch, col, all_rows: bool):
     finally:
         tab.destroy()
     G = fin["n_groups"]
-    out = batch.take(first.view(torch.int64))
+    first64 = first.view(torch.int64)
+    out = batch.take(first64)
     for c, s in zip(sums, agg_t):
         out.data[c.Name.lower()] = _wrap_sum(c, s)
+    if fsums and G:
+        kt = tensors[key_idx]
+        kb = kt if kt.dim() == 2 else kt.view(torch.uint8).view(-1, kt.element_size())
+        perm = engine.sort_perm([(kb[:n], False, _abi.KIND_BYTES)], n, valid=valid)
+        ctx = engine.context()
+        from .columns import torch_dtype
+        for c in fsums:
+            v = batch[c.Name]
+            acc = torch.empty(max(1, n), dtype=torch.float64, device=dev)
+            ctx.check(ctx.L.igx_segment_fsum(ctx.h, engine.ptr(kb), kb.stride(0), kb.shape[1], engine.ptr(perm), n,
+                                             engine.ptr(valid), engine.ptr(v), v.element_size(), engine.ptr(acc)))
+            out.data[c.Name.lower()] = acc[first64].to(torch_dtype(c.kind))
     out.valid = None
     return out, first
 

@@ -764,7 +764,9 @@ def _flatten(vals, sum_cols):
         for name, kind in sum_cols.items():
             cls, w = KIND_CLASS[kind]
             if cls == "float":
-                base[name] = base[name] + v[name]
+                # field.SetFloat(field.Float() + cur.Float()): a float32 field rounds every add
+                s = float(base[name]) + float(v[name])
+                base[name] = float(np.float32(s)) if w == 4 else s
             else:
                 s = int(base[name]) + int(v[name])
                 s &= (1 << (8 * w)) - 1
