@@ -143,8 +143,8 @@ sort_perm_kinds = sort_perm
 class Table:
     """igx_table: keyed aggregation with first-occurrence tracking."""
 
-    def __init__(self, key_widths, aggs, capacity):
-        self.ctx = context()
+    def __init__(self, key_widths, aggs, capacity, ctx=None):
+        self.ctx = context() if ctx is None else ctx
         kw = (C.c_uint32 * len(key_widths))(*key_widths)
         ca = (Agg * max(1, len(aggs)))(*aggs)
         h = C.c_void_p()

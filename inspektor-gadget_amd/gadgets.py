@@ -102,7 +102,7 @@ class _TopTracer:
     SORT_SRC: Dict[str, tuple] = {}
     SortByDefault: list = []
 
-    def __init__(self, MaxRows=_top.MaxRowsDefault, SortBy=None, capacity=1 << 20, Interval=1):
+    def __init__(self, MaxRows=_top.MaxRowsDefault, SortBy=None, capacity=1 << 20, Interval=1, ctx=None):
         self.MaxRows = MaxRows
         self.SortBy = list(self.SortByDefault if SortBy is None else SortBy)
         self.Interval = Interval
@@ -113,7 +113,7 @@ class _TopTracer:
         for kind, vcol, ccol, cval, ow, div in self.AGGS:
             aggs.append(_abi.Agg(kind, 0 if vcol is None else self.ev_index[vcol],
                                  _abi.NO_COL if ccol is None else self.ev_index[ccol], ow, cval, div))
-        self.table = engine.Table(widths, aggs, capacity)
+        self.table = engine.Table(widths, aggs, capacity, ctx=ctx)
         self.key_off = {}
         o = 0
         for k in self.KEY:
@@ -444,6 +444,103 @@ class TopBlockIOTracer(_TopTracer):
 def rwflag_of(cmd_flags):
     """biotop.bpf.c:106: !!((cmd_flags & REQ_OP_MASK) == REQ_OP_WRITE) (host helper)."""
     return int((int(cmd_flags) & 0xFF) == REQ_OP_WRITE)
+
+
+# ------------------------------------------------------------------------------------
+# streaming interval mode (SURVEY.md §8(f) row 2)
+# ------------------------------------------------------------------------------------
+class StreamingTopTracer:
+    """The top tracers' run loop (e.g. pkg/gadgets/top/tcp/tracer/tracer.go:228-265: a
+    ticker calls nextStats, emits stats[:MaxRows], counts Iterations down) over two device
+    tables.  A tick swaps the tables before draining, so the next interval's events are
+    aggregated into the other table -- on a HIP stream of its own -- while the host sorts,
+    gathers and builds the Stats of the interval that just closed (the BPF map keeps taking
+    events while nextStats walks and deletes it).
+
+    cls: a _TopTracer subclass; kw: its constructor arguments (MaxRows, SortBy, capacity,
+    filter options).  Events get global indices continuing across intervals."""
+
+    def __init__(self, cls, Iterations=0, device=None, **kw):
+        torch = torch_mod()
+        from .runtime import Context
+        dev = torch.cuda.current_device() if device is None else device
+        self.Iterations = Iterations
+        self.count = Iterations
+        self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        self.ctxs = [Context(dev, stream=s) for s in self.streams]
+        self.tracers = []
+        for s, c in zip(self.streams, self.ctxs):
+            with torch.cuda.stream(s):
+                self.tracers.append(cls(ctx=c, **kw))
+        self.cur = 0
+        self.next_idx = 0
+        self.done = False
+
+    def feed(self, events: dict, n: Optional[int] = None):
+        """Events of the current interval (device tensors made on torch's current stream)."""
+        torch = torch_mod()
+        tr, s = self.tracers[self.cur], self.streams[self.cur]
+        s.wait_stream(torch.cuda.current_stream())
+        n = int(events[tr.KEY[0]].shape[0]) if n is None else n
+        with torch.cuda.stream(s):
+            tr.feed(events, n, base_idx=self.next_idx)
+        for t in events.values():
+            t.record_stream(s)           # the caller's tensors stay alive for the update
+        self.next_idx += n
+
+    def tick(self):
+        """ticker.C: the interval ends -> top.Event with stats[:MaxRows]; None after the
+        last iteration."""
+        if self.done:
+            return None
+        torch = torch_mod()
+        closed = self.cur
+        self.cur ^= 1                    # later feeds go to the other table
+        with torch.cuda.stream(self.streams[closed]):
+            ev = self.tracers[closed].NextEvent()
+        if self.Iterations > 0:
+            self.count -= 1
+            self.done = self.count == 0
+        return ev
+
+    def run(self, intervals):
+        """Generator over intervals (each an iterable of event batches): interval k+1's
+        updates are enqueued before the host blocks on interval k's drain."""
+        pending = False
+        for batches in intervals:
+            if pending:
+                # enqueue this interval's batches into the fresh table, then drain the old one
+                closed = self.cur ^ 1
+                for b in batches:
+                    self.feed(b)
+                torch = torch_mod()
+                with torch.cuda.stream(self.streams[closed]):
+                    ev = self.tracers[closed].NextEvent()
+                yield ev
+                if self.Iterations > 0:
+                    self.count -= 1
+                    if self.count == 0:
+                        return
+            else:
+                for b in batches:
+                    self.feed(b)
+            self.cur ^= 1
+            pending = True
+        if pending:
+            yield self.tick_closed()
+
+    def tick_closed(self):
+        torch = torch_mod()
+        closed = self.cur ^ 1
+        with torch.cuda.stream(self.streams[closed]):
+            return self.tracers[closed].NextEvent()
+
+    def destroy(self):
+        for t in self.tracers:
+            t.destroy()
+        for c in self.ctxs:
+            c.close()
+
 
 
 # ------------------------------------------------------------------------------------

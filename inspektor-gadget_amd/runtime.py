@@ -24,7 +24,7 @@ class Context:
     """igx_open / igx_close wrapper.  All calls are enqueued on torch's current stream of
     the context's device, so torch ops and igx kernels are ordered with no extra syncs."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, stream=None):
         torch = torch_mod()
         if not torch.cuda.is_available():
             raise IgxError(-2, "no GPU visible: the igx path runs only on MI355X (gfx950)")
@@ -35,11 +35,13 @@ class Context:
         if rc:
             raise IgxError(rc, "igx_open failed (gfx950 GPU required)")
         self.h = h
+        self.stream = stream       # a fixed torch stream (None: follow torch's current one)
         self.bind_stream()
 
     def bind_stream(self, stream=None):
         torch = torch_mod()
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        s = stream if stream is not None else (self.stream if self.stream is not None
+                                               else torch.cuda.current_stream(self.device))
         self.check(self.L.igx_set_stream(self.h, C.c_void_p(s.cuda_stream)))
 
     def check(self, rc):

@@ -403,3 +403,39 @@ def test_trace_open_pipeline_from_samples(oracle, igx, torch):
     assert out.n == len(sel) > 0
     assert np.array_equal(H.host(out["pid"]), ev["pid"][sel][perm])
     assert np.array_equal(H.host(out["path"]), ev["path"][sel][perm])
+
+
+def test_streaming_intervals_double_buffered(oracle, igx, torch, G):
+    """StreamingTopTracer (tracer.go:228-265 over two device tables on two HIP streams):
+    each interval's Event equals a one-shot tracer over that interval's events; global
+    event indices continue across intervals; Iterations stops the loop."""
+    H = igx.columns
+    Gk = 4000
+    cdf = oracle.zipf_cdf(Gk, 1.1)
+    intervals, bases = [], []
+    base = 0
+    for k in range(4):
+        n1, n2 = 60_000 + 1000 * k, 40_000
+        e1 = _dev(H, oracle.gen_tcp(0xC2, k, Gk, cdf, base, n1))
+        e2 = _dev(H, oracle.gen_tcp(0xC2, k, Gk, cdf, base + n1, n2))
+        intervals.append([e1, e2])
+        bases.append(base)
+        base += n1 + n2
+    st = G.StreamingTopTracer(G.TopTcpTracer, MaxRows=25, SortBy=["-sent", "-recv"], capacity=2 * Gk)
+    got = list(st.run(intervals))
+    st.destroy()
+    assert len(got) == 4
+    for k, ev in enumerate(got):
+        one = G.TopTcpTracer(MaxRows=25, SortBy=["-sent", "-recv"], capacity=2 * Gk)
+        for b in intervals[k]:
+            one.feed(b)
+        want = one.NextEvent()
+        one.destroy()
+        assert len(ev.Stats) == len(want.Stats) == 25
+        for a, b in zip(ev.Stats, want.Stats):
+            assert a.FirstIndex == b.FirstIndex + bases[k]
+            a.FirstIndex = b.FirstIndex
+            assert a == b
+    st2 = G.StreamingTopTracer(G.TopTcpTracer, Iterations=2, MaxRows=5, capacity=2 * Gk)
+    assert len(list(st2.run(intervals))) == 2
+    st2.destroy()
