@@ -266,8 +266,10 @@ int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete lo
 int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uint32_t k,
                      uint32_t *out_slots);
 int igx_groupby_destroy(igx_table *t);
-/* Diagnostics only (IGX_GB_DEBUG env bit 3): LDS-cache hits / misses since the last call. */
-int igx_groupby_debug_counts(igx_table *t, uint64_t *out4);
+/* Diagnostics only (IGX_GB_DEBUG env): out8[0..1] LDS-cache hits / misses (bit 3); out8[4..7]
+ * sleep counts of loaders on a full miss ring, probers on an empty one, probers on a full
+ * update ring, the idle server (bit 16).  Counters since the last call. */
+int igx_groupby_debug_counts(igx_table *t, uint64_t *out8);
 
 /* ---- advise network-policy -------------------------------------------------------------- */
 /* keep[i] = 1 iff the advisor would consider event i (advisor.go:279-292): type == normal

@@ -96,6 +96,7 @@ struct GbArgs {
     uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
     uint32_t npred;
     uint32_t lds_entries;   // E (8 x sets)
+    uint32_t sm;            // 1: state-machine probers (IGX_GB_PROBER=0: batch probers)
     uint32_t admit_mask;    // 1: LDS admission on a key's second miss (ghost_admit), 0: on the first
     uint32_t nl;            // loader waves (1..14)
     // input
@@ -652,11 +653,13 @@ __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32
     if ((threadIdx.x & 63) == leader) base = atomicAdd(&r.ctl[0], total);
     base = __shfl(base, (int)leader);
     // wait for room: the server frees entries as it issues them
-    for (uint32_t spins = 0;
-         base + total - __hip_atomic_load(&r.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > ARING;) {
+    uint32_t spins = 0;
+    for (; base + total - __hip_atomic_load(&r.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > ARING;) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); return; }   // never expected: fail, do not hang
     }
+    if ((a.dbg & 65536u) && spins && (threadIdx.x & 63) == leader)
+        atomicAdd(a.dbg_cnt + 6, 1ull * spins);   // prober: update ring full
     uint32_t off = base;
     const uint64_t lt = lanemask_lt();
 #pragma unroll
@@ -683,6 +686,7 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
                 __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == head)
                 break;
             __builtin_amdgcn_s_sleep(2);   // idle until the probers push or finish (no limit:
+            if (DBG && (a.dbg & 65536u) && lane == 0) atomicAdd(a.dbg_cnt + 7, 1ull);   // server idle
             continue;                      // they bound their own waits)
         }
         const uint32_t n = min(t - head, 64u);
@@ -725,6 +729,7 @@ struct MissRing {
     uint32_t *seq;    // MRING
     uint32_t *ctl;    // [0] tail (reservations), [1] head (claims), [2] loader waves done
     uint32_t *err;
+    unsigned long long *waits;   // diagnostics (IGX_GB_DEBUG bit 16): sleep counts, else null
 };
 
 template <int KW, int NA>
@@ -737,10 +742,12 @@ __device__ __forceinline__ void miss_push(const MissRing<KW, NA> &m, const uint3
     base = __shfl(base, (int)leader);
     const uint32_t p = base + (uint32_t)__popcll(active & lanemask_lt());
     uint32_t *sq = &m.seq[p % MRING];
-    for (uint32_t spins = 0; __hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p;) {
+    uint32_t spins = 0;
+    for (; __hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p;) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > SPIN_LIMIT) { atomicOr(m.err, 16u); return; }
     }
+    if (m.waits && spins) atomicAdd(m.waits + 4, (unsigned long long)spins);   // loader: ring full
     uint4 *cl = m.cell + (uint64_t)(p % MRING) * MissRing<KW, NA>::EQ;
 #pragma unroll
     for (int q = 0; q < MissRing<KW, NA>::KQ; ++q)
@@ -790,6 +797,168 @@ __device__ __forceinline__ void read_cell(const MissRing<KW, NA> &m, uint32_t p,
     }
 }
 
+// The state-machine prober: every lane owns one miss and advances it by one step per round
+// trip, so a lane that has to claim a record (CAS, then key / value stores, then `ready`)
+// does not hold the other 63 lanes for the extra round trips.  Per iteration: free lanes
+// take cells from the miss ring; lanes in PROBE load their slot's record, lanes in CASQ
+// issue their claim; one wait covers all of it (and the previous iteration's stores); then
+// PUB lanes publish, CAS lanes act on the result, PROBE lanes read their record.
+// States: FREE -> PROBE -> (found: FREE) | (empty: CASQ -> CAS -> (won: PUB -> FREE) |
+// (lost: PROBE)).
+template <int KW, int NA, bool DBG>
+__device__ __forceinline__ void finish_miss(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
+                                            const MissRow<KW, NA> &x, uint32_t gs, uint64_t first_ins) {
+    const int ad = ghost_admit<KW>(a, c, x.h) ? lds_adopt<KW>(c, x.k, x.h, gs) : -1;
+    if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x.v, x.gidx);
+    else ring_push<NA>(a, r, gs, x.v, x.gidx, first_ins);
+}
+
+template <int KW, int NA, bool DBG>
+__device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
+                                          const MissRing<KW, NA> &m, uint32_t lane) {
+    constexpr uint32_t KOFF = koff_of(KW);
+    constexpr int NQ = probe_quads<KW>();
+    constexpr uint32_t FREE = 0, PROBE = 1, CASQ = 2, PUB = 3;
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
+    MissRow<KW, NA> x;
+    uint32_t st = FREE, s = 0, probes = 0, tries = 0, reread = 0;
+    uint64_t expect = 0;
+    for (uint32_t idle = 0;;) {
+        // 1. refill the free lanes with cells the loaders have reserved
+        const uint64_t fm = __ballot(st == FREE);
+        bool drained = false;
+        if (fm) {
+            const uint32_t tail = __hip_atomic_load(&m.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const bool done = __hip_atomic_load(&m.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == a.nl;
+            const uint32_t head = __hip_atomic_load(&m.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t avail = (int32_t)(tail - head) > 0 ? tail - head : 0u;
+            const uint32_t want = min((uint32_t)__popcll(fm), avail);
+            drained = done && avail == 0;
+            if (want) {
+                const uint32_t leader = (uint32_t)__ffsll((long long)fm) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&m.ctl[1], want);
+                base = __shfl(base, (int)leader);
+                const uint32_t rank = (uint32_t)__popcll(fm & lanemask_lt());
+                if (st == FREE && rank < want) {
+                    const uint32_t p = base + rank;
+                    uint32_t *sq = &m.seq[p % MRING];
+                    bool have = true;
+                    for (uint32_t spins = 0;
+                         __hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p + 1;) {
+                        if (__hip_atomic_load(&m.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == a.nl &&
+                            p >= __hip_atomic_load(&m.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            have = false;   // over-claimed past the end of a finished stream
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have = false; break; }
+                    }
+                    if (have) {
+                        read_cell<KW, NA>(m, p, x);
+                        __hip_atomic_store(sq, p + MRING, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        uint32_t gs = SLOT_OVF;
+                        const int slot = lds_lookup<KW>(c, x.k, x.h, gs);   // adopted meanwhile?
+                        if (slot >= 0) {
+                            lds_accumulate<KW, NA>(a, c, slot, x.v, x.gidx);
+                        } else {
+                            st = PROBE;
+                            s = (uint32_t)((x.h >> 17) & a.mask);
+                            probes = 0;
+                            tries = 0;
+                            reread = 0;
+                        }
+                    }
+                }
+            }
+        }
+        const uint64_t busy = __ballot(st != FREE);
+        if (!busy) {
+            if (drained) break;
+            __builtin_amdgcn_s_sleep(1);   // waiting for misses: as long as the stream lasts
+            if (++idle > SPIN_LIMIT) { atomicOr(a.err, 16u); break; }
+            continue;
+        }
+        idle = 0;
+        // 2. issue this round trip's loads and claims
+        const uint64_t tag = (x.h & ~EP_MAX) | a.ep;
+        uint8_t *rec = a.krec + (uint64_t)s * a.krec_len;
+        uint32_t d[NQ * 4];
+        uint64_t cas_old = 0;
+        const bool probed = st == PROBE;   // only these lanes have a record in d this round
+        if (probed) load_rec<NQ>(rs, s * a.krec_len, d);
+        if (st == CASQ)
+            cas_old = atomicCAS(reinterpret_cast<unsigned long long *>(rec + KOFF), (unsigned long long)expect,
+                                (unsigned long long)tag);
+        // 3. one wait: probe data, claims, and the previous iteration's stores
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // 4. publish the records claimed last iteration (their stores are now complete)
+        if (st == PUB) {
+            st_agent(reinterpret_cast<uint64_t *>(rec + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
+            atomicOr(a.occ + (s >> 5), 1u << (s & 31));
+            finish_miss<KW, NA, DBG>(a, c, r, x, s, x.gidx);
+            st = FREE;
+        }
+        // 5. claims: won -> write key and value record now, publish next iteration
+        if (st == CASQ) {
+            if (cas_old == expect) {
+#pragma unroll
+                for (int w = 0; w < KW; w += 2) {
+                    if (w + 1 < KW)
+                        st_agent(reinterpret_cast<uint64_t *>(rec + 4 * w), (uint64_t)x.k[w] | ((uint64_t)x.k[w + 1] << 32));
+                    else
+                        st_agent(reinterpret_cast<uint32_t *>(rec + 4 * w), x.k[w]);
+                }
+                uint64_t *vr = a.vrec + (uint64_t)s * a.vrec_words;
+                st_agent(vr, x.gidx);
+                for (uint32_t q = 1; q < a.vrec_words; ++q) st_agent(vr + q, 0ull);
+                st = PUB;
+            } else if (cas_old == tag) {
+                st = PROBE;   // lost to a claim of the same hash: read its key once `ready` is set
+                if (++tries > (1u << 18)) { atomicOr(a.err, 2u); st = FREE; }
+            } else {
+                st = PROBE;   // lost to another key (the CAS saw the current tag): next slot
+                reread = 0;
+                s = (uint32_t)((s + 1) & a.mask);
+                if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
+            }
+        }
+        // 6. probe results (lanes that lost a claim in step 5 read their record next round)
+        if (probed && st == PROBE) {
+            const uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
+            const uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
+            if ((t & EP_MAX) != a.ep) {
+                expect = t;          // empty in this interval: claim it next round trip
+                st = CASQ;
+                if (++tries > (1u << 18)) { atomicOr(a.err, 2u); st = FREE; }
+            } else if (t == tag) {
+                if (!ready_ok(ready, a.ep)) {
+                    if (++tries > (1u << 18)) { atomicOr(a.err, 2u); st = FREE; }   // the claimer is still writing
+                } else {
+                    bool eq = true;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) eq = eq && (d[w] == x.k[w]);
+                    if (eq) {
+                        finish_miss<KW, NA, DBG>(a, c, r, x, s, (ready & READY_IDX) - 1);
+                        st = FREE;
+                    } else if (!reread) {
+                        reread = 1;  // the key quads may predate `ready`: read once more
+                        ++tries;
+                    } else {
+                        reread = 0;
+                        s = (uint32_t)((s + 1) & a.mask);
+                        if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
+                    }
+                }
+            } else {
+                reread = 0;
+                s = (uint32_t)((s + 1) & a.mask);
+                if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
+            }
+        }
+    }
+}
+
 template <int KW, int NA, bool DBG>
 __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
                                        const MissRing<KW, NA> &m, uint32_t lane) {
@@ -815,6 +984,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                     if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have[j] = false; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);   // waiting for misses: as long as the stream lasts
+                if (DBG && m.waits) atomicAdd(m.waits + 5, 1ull);              // prober: ring empty
             }
             if (have[j]) {
                 read_cell<KW, NA>(m, p, x[j]);
@@ -880,6 +1050,7 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     m.seq = reinterpret_cast<uint32_t *>(m.cell + MRING * MissRing<KW, NA>::EQ);
     m.ctl = ring_ctl + 4;
     m.err = a.err;
+    m.waits = (DBG && (a.dbg & 65536u)) ? a.dbg_cnt : nullptr;
     c.ghost = m.seq + MRING;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
@@ -897,13 +1068,15 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     if (wave == NWAVES - 1) {
         ring_serve<DBG>(a, r, lane);
     } else if (wave >= a.nl) {
-        prober<KW, NA, DBG>(a, c, r, m, lane);
+        if (a.sm) prober_sm<KW, NA, DBG>(a, c, r, m, lane);
+        else prober<KW, NA, DBG>(a, c, r, m, lane);
         if (lane == 0) atomicAdd(&r.ctl[2], 1u);
     } else {
         const uint32_t PTB = a.nl * 64;   // rows per workgroup step
         const uint64_t stride = (uint64_t)gridDim.x * PTB;
         uint64_t base = (uint64_t)blockIdx.x * PTB + wave * 64;
         RowRaw<L, NA> R;
+        uint32_t nmiss = 0;
         if (base < a.n) issue_row<L, NA>(a, min(base + lane, a.n - 1), R);
         for (; base < a.n; base += stride) {
             const uint64_t row = base + lane;
@@ -916,17 +1089,22 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
                 if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live
                 ok = false;
             }
-            if (!ok) continue;
-            uint32_t gs = SLOT_OVF;
-            const int slot = lds_lookup<KW>(c, k, h, gs);
-            if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
-            if (slot >= 0) {
-                if (!(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
-                    lds_accumulate<KW, NA>(a, c, slot, v, row_gidx(a, row));
-            } else if (!(DBG && (a.dbg & 2u))) {
-                miss_push<KW, NA>(m, k, h, row_gidx(a, row), v);
+            if (ok) {
+                uint32_t gs = SLOT_OVF;
+                const int slot = lds_lookup<KW>(c, k, h, gs);
+                if (DBG && (a.dbg & 8u)) atomicAdd(a.dbg_cnt + (slot >= 0 ? 0 : 1), 1ull);
+                if (slot >= 0) {
+                    if (!(DBG && (a.dbg & 512u)))   // diagnostics: bit9 no LDS accumulate
+                        lds_accumulate<KW, NA>(a, c, slot, v, row_gidx(a, row));
+                } else if (!(DBG && (a.dbg & 2u))) {
+                    miss_push<KW, NA>(m, k, h, row_gidx(a, row), v);
+                    ++nmiss;
+                }
             }
         }
+        // LDS misses of this interval (err block + 8): the host picks the prober for the next one
+        for (int o = 32; o > 0; o >>= 1) nmiss += __shfl_xor(nmiss, o);
+        if (lane == 0 && nmiss) atomicAdd(reinterpret_cast<unsigned long long *>(a.err + 2), (unsigned long long)nmiss);
         if (lane == 0) atomicAdd(&m.ctl[2], 1u);
     }
 
@@ -1070,6 +1248,8 @@ struct igx_table {
     uint64_t occ_words = 0;
     uint64_t ep = 0;             // current epoch (1..EP_MAX)
     uint64_t *n_groups = nullptr;
+    uint64_t rows_fed = 0;       // rows given to update since the last reset
+    bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[8] = {};       // IP text of the groups, per IGX_TSRC_IPTEXT sort key
@@ -1189,7 +1369,8 @@ extern "C" int igx_groupby_reset(igx_table *t) {
         t->ep = 1;
     }
     IGX_HIP(ctx, hipMemsetAsync(t->occ, 0, t->occ_words * 4, ctx->stream));
-    IGX_HIP(ctx, hipMemsetAsync(t->err, 0, 4, ctx->stream));
+    IGX_HIP(ctx, hipMemsetAsync(t->err, 0, 16, ctx->stream));   // error bits + LDS-miss count
+    t->rows_fed = 0;
     t->host_groups = 0;
     return IGX_OK;
 }
@@ -1258,6 +1439,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     if (nrows == 0) return IGX_OK;
     if (!cols || !key_cols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: null columns");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "groupby_update: more than 2^32 rows in one call");
+    t->rows_fed += nrows;
     GbArgs a{};
     uint32_t w = 0;
     for (uint32_t k = 0; k < t->nkeys; ++k) {
@@ -1409,6 +1591,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         if (v >= 1 && v <= NWAVES - 2) a.nl = (uint32_t)v;
     }
     a.admit_mask = 1;
+    a.sm = t->prefer_sm ? 1u : 0u;
+    if (const char *d = std::getenv("IGX_GB_PROBER")) a.sm = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     if (const char *d = std::getenv("IGX_GB_ADMIT")) a.admit_mask = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     a.dbg_cnt = t->dbg_cnt;
     const uint64_t want = (nrows + GTB - 1) / GTB;
@@ -1452,14 +1636,18 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
                        t->tile_cnt, t->groups);
     IGX_HIP(ctx, hipGetLastError());
     uint64_t *h;
-    int rc = igx_pinned(ctx, 16, reinterpret_cast<void **>(&h));
+    int rc = igx_pinned(ctx, 24, reinterpret_cast<void **>(&h));
     if (rc) return rc;
     IGX_HIP(ctx, hipMemcpyAsync(h, t->n_groups, 8, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipMemcpyAsync(reinterpret_cast<uint32_t *>(h) + 2, t->err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(h + 1, t->err, 16, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t ng = h[0];
     const uint32_t err = reinterpret_cast<uint32_t *>(h)[2];
+    const uint64_t misses = h[2];
     t->host_groups = ng;
+    // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
+    // go faster with the state-machine probers; hit-heavy ones with the batch probers.
+    if (t->rows_fed >= 1000000) t->prefer_sm = misses * 10 > t->rows_fed * 7;
     if (view) {
         view->n_groups = ng;
         view->n_slots = t->nslots;
@@ -1563,10 +1751,10 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.
-extern "C" int igx_groupby_debug_counts(igx_table *t, uint64_t *out4) {
-    if (!t || !out4) return IGX_EINVAL;
+extern "C" int igx_groupby_debug_counts(igx_table *t, uint64_t *out8) {
+    if (!t || !out8) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    IGX_HIP(ctx, hipMemcpyAsync(out4, t->dbg_cnt, 32, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(out8, t->dbg_cnt, 64, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     IGX_HIP(ctx, hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream));
     return IGX_OK;

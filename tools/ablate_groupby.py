@@ -25,6 +25,7 @@ def main():
     p.add_argument("--zipf", type=float, default=1.1)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--variants", default="0,1,2,4,8")
+    p.add_argument("--noreset", action="store_true", help="keep the table between launches (no new keys after the first)")
     a = p.parse_args()
     variants = [int(x) for x in a.variants.split(",")]
     import torch
@@ -43,18 +44,24 @@ def main():
     for r in range(a.rounds):
         for v in variants:
             os.environ["IGX_GB_DEBUG"] = str(v)
-            tab.reset()
+            if not a.noreset:
+                tab.reset()
+            elif r == 0 and v == variants[0]:
+                tab.update(cols, list(range(8)), N, 0)   # populate: later launches find every key
             e0.record()
             tab.update(cols, list(range(8)), N, 0)
             e1.record()
             torch.cuda.synchronize()
             res.setdefault(v, []).append(e0.elapsed_time(e1))
-            if v == 8:
-                cnt = (C.c_uint64 * 4)()
+            if v & (8 | 65536):
+                cnt = (C.c_uint64 * 8)()
                 tab.ctx.check(tab.ctx.L.igx_groupby_debug_counts(tab.h, cnt))
-                res.setdefault("hits_misses", []).append([cnt[0], cnt[1]])
+                if v & 8:
+                    res.setdefault("hits_misses", []).append([cnt[0], cnt[1]])
+                if v & 65536:
+                    res.setdefault("waits_lfull_pempty_ufull_sidle", []).append([cnt[4], cnt[5], cnt[6], cnt[7]])
     os.environ.pop("IGX_GB_DEBUG", None)
-    out = {str(k): (float(np.median(v)) if k != "hits_misses" else v[-1]) for k, v in res.items()}
+    out = {str(k): (float(np.median(v)) if not isinstance(k, str) else v[-1]) for k, v in res.items()}
     out.update({"events": N, "keys": G, "zipf": a.zipf})
     print(json.dumps(out))
     tab.destroy()
