@@ -35,7 +35,7 @@
 // their own input bytes plus LDS atomics.  A miss is resolved at once, while its row is in
 // registers: HBM probe, adoption of a free LDS entry when its set has one, and otherwise
 // its HBM updates go to the server wave through an LDS ring (see "HBM atomics through an
-// LDS ring").  Fifteen waves stream rows, the sixteenth issues the ring's atomics.  The
+// LDS ring").  Eight waves stream rows, seven resolve misses, the sixteenth issues the atomics.  The
 // cache is committed with HBM atomics at the end.
 #include <cstdlib>
 #include <type_traits>
@@ -622,7 +622,7 @@ constexpr uint32_t WHAT_MIN = 15;           // entry kind: atomicMin on `first`
 // wave roles in a workgroup: a.nl loaders stream rows, the next 15 - a.nl waves (probers)
 // resolve LDS misses against HBM, and the last wave serves the HBM-update ring
 constexpr uint32_t NWAVES = GTB / 64;
-constexpr uint32_t NL_DEFAULT = 10;
+constexpr uint32_t NL_DEFAULT = 8;    // loader waves (7 probers + 1 server): tools/gpu/nl_cfg.sh
 
 struct Ring {
     uint2 *lo;            // {slot, (lap << 4) | what}
