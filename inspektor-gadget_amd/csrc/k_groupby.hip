@@ -96,6 +96,7 @@ struct GbArgs {
     uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
     uint32_t npred;
     uint32_t lds_entries;   // E (8 x sets)
+    uint32_t direct;        // 1: probers issue their HBM atomics; the server wave probes too
     uint32_t sm;            // 1: state-machine probers (IGX_GB_PROBER=0: batch probers)
     uint32_t admit_mask;    // 1: LDS admission on a key's second miss (ghost_admit), 0: on the first
     uint32_t nl;            // loader waves (1..14)
@@ -637,6 +638,13 @@ __device__ __forceinline__ uint32_t ring_lap(uint32_t p) { return (p / ARING + 1
 template <int NA>
 __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32_t gs, const uint64_t (&v)[NA],
                                           uint64_t gidx, uint64_t first_ins) {
+    if (a.direct) {   // the prober issues its own atomics (no server wave)
+#pragma unroll
+        for (int x = 0; x < NA; ++x)
+            if (x < (int)a.naggs && v[x]) gadd(rec_agg(a, gs, x), (unsigned long long)v[x]);
+        if (gidx < first_ins) gmin(rec_first(a, gs), (unsigned long long)gidx);
+        return;
+    }
     bool has[NA + 1];
     uint64_t mask[NA + 1];
     uint32_t total = 0;
@@ -1065,7 +1073,7 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     if (threadIdx.x < 8) ring_ctl[threadIdx.x] = 0;
     __syncthreads();
 
-    if (wave == NWAVES - 1) {
+    if (wave == NWAVES - 1 && !a.direct) {
         ring_serve<DBG>(a, r, lane);
     } else if (wave >= a.nl) {
         if (a.sm) prober_sm<KW, NA, DBG>(a, c, r, m, lane);
@@ -1592,6 +1600,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     }
     a.admit_mask = 1;
     a.sm = t->prefer_sm ? 1u : 0u;
+    a.direct = 0;
+    if (const char *d = std::getenv("IGX_GB_DIRECT")) a.direct = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     if (const char *d = std::getenv("IGX_GB_PROBER")) a.sm = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     if (const char *d = std::getenv("IGX_GB_ADMIT")) a.admit_mask = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     a.dbg_cnt = t->dbg_cnt;
