@@ -308,3 +308,54 @@ def test_merge_partials_on_device(oracle, E, H, igx, torch):
     perm = oracle.go_sort_entries([(o[1][1].astype(np.uint32), "uint32", True)], len(o[0]))
     assert np.array_equal(got_first, o[2][perm.astype(np.int64)][:20])
     tab.destroy()
+
+
+@pytest.mark.parametrize("prober", ["batch", "state-machine", "adaptive"])
+@pytest.mark.parametrize("layout", ["tcp", "file", "netpolicy"])
+def test_both_prober_forms(oracle, E, H, igx, torch, prober, layout, monkeypatch):
+    """Both forms of the miss-resolving waves (batch / state-machine) give the same exact
+    table; 'adaptive' lets a miss-heavy first interval switch the table to the
+    state-machine form for the second (the kernel's LDS-miss count, read at finalize)."""
+    import os
+    A = igx._abi
+    if prober != "adaptive":
+        monkeypatch.setenv("IGX_GB_PROBER", "1" if prober == "state-machine" else "0")
+    else:
+        monkeypatch.delenv("IGX_GB_PROBER", raising=False)
+    n = 1_200_000
+    if layout == "tcp":
+        G = 200_000                                       # near-uniform: most rows miss LDS
+        ev_h = oracle.gen_tcp(0xB7, 0, G, oracle.zipf_cdf(G, 0.2), 0, n)
+        names, widths = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family"), \
+            [16, 16, 8, 4, 16, 2, 2, 2]
+        aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
+        extra = ["size", "dir"]
+        oaggs = [{"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 0},
+                 {"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 1}]
+    elif layout == "file":
+        G = 300_000
+        ev_h = oracle.gen_file(0xC5, 0, G, oracle.zipf_cdf(G, 0.3), 0, n)
+        names, widths = ("inode", "dev", "pid", "tid"), [8, 4, 4, 4]
+        aggs = [A.Agg(A.AGG_COUNT, 0, 5, 8, 0), A.Agg(A.AGG_SUM, 4, 5, 8, 0),
+                A.Agg(A.AGG_COUNT, 0, 5, 8, 1), A.Agg(A.AGG_SUM, 4, 5, 4, 1)]
+        extra = ["count", "op"]
+        oaggs = [{"kind": "count", "cond": ev_h["op"], "cond_val": 0},
+                 {"kind": "sum", "val": ev_h["count"], "cond": ev_h["op"], "cond_val": 0},
+                 {"kind": "count", "cond": ev_h["op"], "cond_val": 1},
+                 {"kind": "sum", "val": ev_h["count"], "cond": ev_h["op"], "cond_val": 1, "out_width": 4}]
+    else:
+        ev_h = oracle.gen_np(0xC4, 5_000, 50_000, 0, n)
+        names, widths = ("src", "pkt", "peer", "port"), [4, 1, 4, 2]
+        aggs = [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)]
+        extra = []
+        oaggs = [{"kind": "count"}]
+        G = n
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    cols = [ev[k] for k in list(names) + extra]
+    tab = E.Table(widths, aggs, min(2 * G, n))
+    o = oracle.groupby(oracle.pack_cols(ev_h, names), oaggs)
+    for _ in range(2):                                   # two intervals
+        tab.update(cols, list(range(len(names))), n, 0)
+        _check(E, H, tab, widths, *o)
+        tab.reset()
+    tab.destroy()
