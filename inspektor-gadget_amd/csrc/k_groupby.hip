@@ -118,7 +118,7 @@ struct GbArgs {
     uint64_t mask;
     uint32_t max_probe;
     // diagnostics (IGX_GB_DEBUG; compiled into the top-tcp key's debug kernel only):
-    // bit0 stop after load+hash, bit1 drop LDS misses, bit2 drop HBM atomics, bit3 count
+    // bit0 stop after load+hash, bit1 drop LDS misses, bit10 probers drop the cells they take, bit2 drop HBM atomics, bit3 count
     // hits/misses, bit8 no HBM probe (a hash-derived slot), bit9 no LDS accumulate on hits
     uint32_t dbg;
     unsigned long long *dbg_cnt;
@@ -1003,6 +1003,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
 #pragma unroll
         for (int j = 0; j < PB; ++j) any = any || have[j];
         if (__ballot(any) == 0) break;
+        if (DBG && (a.dbg & 1024u)) continue;   // diagnostics: hand-off only (cells taken, dropped)
         bool probe[PB];
         uint32_t d[PB][probe_quads<KW>() * 4];
 #pragma unroll
