@@ -18,10 +18,17 @@
 // its neighbour.  u16 halves the LDS footprint: C3's 4096 keys x 27 slots need two
 // partitions instead of four.  The partitions of a key range run on blocks that share an
 // XCD (blockIdx % 8, speed only) and sweep the same chunks, so the repeated reads are L2
-// hits.  Each lane keeps 8 rows (128 B of loads) in flight per chunk -- the kernel is
+// hits.  Slot window: when all keys x nslots do not fit one partition but keys x W slots
+// do (W >= 8), LDS holds only slots [lo, lo + W) of every key and rows outside the window
+// add to HBM directly (u32 atomics, still exact); lo is picked on the device by a one-
+// workgroup pass over a 64K-row sample (the window with the most rows), so no row is read
+// twice and no host round trip is added.  Latency histograms are narrow in log2 space (C3:
+// lognormal, sigma = 2.2 slots), so the window holds all but ~1e-4 of the rows.
+// Each lane keeps 8 rows (128 B of loads) in flight per chunk -- the kernel is
 // bound by bytes in flight, not by arithmetic.  Small histograms are replicated per wave
 // to spread LDS atomic contention.  Commit: one HBM atomic add per non-zero counter.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "k_common.h"
@@ -44,6 +51,8 @@ struct HistArgs {
     uint8_t dev_idx[DEVTAB];
     uint32_t single;            // ndev == 0: every row is device 0 (the shipped gadget)
     uint32_t ndev, ncont, nslots;
+    uint32_t W;                 // slots held in LDS per key (== nslots without a window)
+    const uint32_t *lo;         // device: first LDS slot (null: 0)
     uint32_t P;                 // key partitions
     uint32_t Kp;                // keys per partition
     uint32_t R;                 // LDS replicas
@@ -70,6 +79,7 @@ struct Counter {
     const uint8_t *sidx;
     uint32_t *hr;
     uint32_t kbase;
+    uint32_t lo;
 
     __device__ __forceinline__ void operator()(uint32_t dv, uint32_t ci, int64_t d) const {
         uint32_t di = 0;
@@ -87,12 +97,17 @@ struct Counter {
         const uint64_t v = divide<DIV>((uint64_t)d, a.divisor);
         uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
         slot = min(slot, a.nslots - 1);
-        const uint32_t idx = kk * a.nslots + slot;
+        const uint32_t ws = slot - lo;
+        if (ws >= a.W) {             // outside the LDS window: straight to HBM
+            atomicAdd(&a.hist[((uint64_t)kbase + kk) * a.nslots + slot], 1u);
+            return;
+        }
+        const uint32_t idx = kk * a.W + ws;
         const uint32_t sh = (idx & 1u) * 16u;
         const uint32_t old = atomicAdd(&hr[idx >> 1], 1u << sh);
         if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {   // this add took it to 0x8000
             atomicSub(&hr[idx >> 1], 0x8000u << sh);
-            atomicAdd(&a.hist[(uint64_t)kbase * a.nslots + idx], 0x8000u);
+            atomicAdd(&a.hist[((uint64_t)kbase + kk) * a.nslots + slot], 0x8000u);
         }
     }
 };
@@ -111,51 +126,95 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     const uint32_t b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const uint32_t p = j % a.P, g = j / a.P;
     const uint32_t cgroup = g * 8 + xcd;
-    const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp};
+    const uint32_t lo = a.lo ? *a.lo : 0u;
+    const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp, lo};
     const uint64_t nchunks = (a.n + CHUNK - 1) / CHUNK;
     uint32_t it = 0;
-    for (uint64_t c = cgroup; c < nchunks; c += a.ngroups) {
-        const uint64_t base = c * CHUNK;
-        if (VEC && base + CHUNK <= a.n) {
-            // lane t covers rows base + 4t .. +3 and base + 4096 + 4t .. +3: every load is
-            // 16 B and a wave's loads are contiguous
-            const uint64_t r0 = base + 4ull * threadIdx.x, r1 = r0 + 4ull * TB;
-            const uint4 dv0 = *reinterpret_cast<const uint4 *>(a.dev + r0);
-            const uint4 dv1 = *reinterpret_cast<const uint4 *>(a.dev + r1);
-            uint4 ci0 = make_uint4(0, 0, 0, 0), ci1 = ci0;
-            if (a.cont) {
-                ci0 = *reinterpret_cast<const uint4 *>(a.cont + r0);
-                ci1 = *reinterpret_cast<const uint4 *>(a.cont + r1);
-            }
-            const longlong2 d0 = *reinterpret_cast<const longlong2 *>(a.delta + r0);
-            const longlong2 d1 = *reinterpret_cast<const longlong2 *>(a.delta + r0 + 2);
-            const longlong2 d2 = *reinterpret_cast<const longlong2 *>(a.delta + r1);
-            const longlong2 d3 = *reinterpret_cast<const longlong2 *>(a.delta + r1 + 2);
-            count(dv0.x, ci0.x, d0.x);
-            count(dv0.y, ci0.y, d0.y);
-            count(dv0.z, ci0.z, d1.x);
-            count(dv0.w, ci0.w, d1.y);
-            count(dv1.x, ci1.x, d2.x);
-            count(dv1.y, ci1.y, d2.y);
-            count(dv1.z, ci1.z, d3.x);
-            count(dv1.w, ci1.w, d3.y);
-        } else {
-#pragma unroll
-            for (int r = 0; r < RPL; ++r) {
-                const uint64_t row = base + (uint64_t)r * TB + threadIdx.x;
-                if (row < a.n) count(a.dev ? a.dev[row] : 0u, a.cont ? a.cont[row] : 0u, a.delta[row]);
-            }
+    // full chunks: 8 rows per lane as 16-B loads (lane t covers rows base + 4t .. +3 and
+    // base + 4096 + 4t .. +3), software-pipelined: the next chunk's loads are in flight
+    // while this one's rows are counted
+    struct Rows { uint4 dv0, dv1, ci0, ci1; longlong2 d0, d1, d2, d3; };
+    auto load = [&](uint64_t base, Rows &R) {
+        const uint64_t r0 = base + 4ull * threadIdx.x, r1 = r0 + 4ull * TB;
+        R.dv0 = *reinterpret_cast<const uint4 *>(a.dev + r0);
+        R.dv1 = *reinterpret_cast<const uint4 *>(a.dev + r1);
+        R.ci0 = make_uint4(0, 0, 0, 0);
+        R.ci1 = R.ci0;
+        if (a.cont) {
+            R.ci0 = *reinterpret_cast<const uint4 *>(a.cont + r0);
+            R.ci1 = *reinterpret_cast<const uint4 *>(a.cont + r1);
         }
-        if (++it % CHUNKS_PER_TILE == 0) __syncthreads();   // tile boundary (see header)
+        R.d0 = *reinterpret_cast<const longlong2 *>(a.delta + r0);
+        R.d1 = *reinterpret_cast<const longlong2 *>(a.delta + r0 + 2);
+        R.d2 = *reinterpret_cast<const longlong2 *>(a.delta + r1);
+        R.d3 = *reinterpret_cast<const longlong2 *>(a.delta + r1 + 2);
+    };
+    const uint64_t nfull = VEC ? a.n / CHUNK : 0;
+    uint64_t c = cgroup;
+    if (c < nfull) {
+        Rows R;
+        load(c * CHUNK, R);
+        for (; c < nfull; c += a.ngroups) {
+            const Rows cur = R;
+            if (c + a.ngroups < nfull) load((c + a.ngroups) * CHUNK, R);
+            count(cur.dv0.x, cur.ci0.x, cur.d0.x);
+            count(cur.dv0.y, cur.ci0.y, cur.d0.y);
+            count(cur.dv0.z, cur.ci0.z, cur.d1.x);
+            count(cur.dv0.w, cur.ci0.w, cur.d1.y);
+            count(cur.dv1.x, cur.ci1.x, cur.d2.x);
+            count(cur.dv1.y, cur.ci1.y, cur.d2.y);
+            count(cur.dv1.z, cur.ci1.z, cur.d3.x);
+            count(cur.dv1.w, cur.ci1.w, cur.d3.y);
+            if (++it % CHUNKS_PER_TILE == 0) __syncthreads();   // tile boundary (see header)
+        }
+    }
+    // the rest (partial chunk, or every chunk when the columns are not 16-B aligned)
+    for (; c < nchunks; c += a.ngroups) {
+        const uint64_t base = c * CHUNK;
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            const uint64_t row = base + (uint64_t)r * TB + threadIdx.x;
+            if (row < a.n) count(a.dev ? a.dev[row] : 0u, a.cont ? a.cont[row] : 0u, a.delta[row]);
+        }
+        if (++it % CHUNKS_PER_TILE == 0) __syncthreads();
     }
     __syncthreads();
     const uint32_t nkeys = a.ndev * a.ncont;
     const uint32_t kbase = p * a.Kp;
     const uint32_t nkeys_here = kbase < nkeys ? min(a.Kp, nkeys - kbase) : 0u;
-    for (uint32_t i = threadIdx.x; i < nkeys_here * a.nslots; i += TB) {
+    for (uint32_t i = threadIdx.x; i < nkeys_here * a.W; i += TB) {
         uint32_t s = 0;
         for (uint32_t r = 0; r < a.R; ++r) s += (h[r * a.rep_words + (i >> 1)] >> ((i & 1u) * 16u)) & 0xFFFFu;
-        if (s) atomicAdd(&a.hist[(uint64_t)kbase * a.nslots + i], s);
+        if (s) atomicAdd(&a.hist[((uint64_t)kbase + i / a.W) * a.nslots + lo + i % a.W], s);
+    }
+}
+
+// The slot window's start: log2 slots of a strided 64K-row sample (devices and containers
+// ignored), then the lo in [0, nslots - W] whose window holds the most sampled rows.
+template <int DIV>
+__global__ __launch_bounds__(TB) void k_hist_window(const int64_t *__restrict__ delta, uint64_t n, uint64_t divisor,
+                                                    uint32_t nslots, uint32_t W, uint32_t *__restrict__ lo_out) {
+    __shared__ uint32_t cnt[64];
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t ns = n < 65536 ? n : 65536;
+    const uint64_t step = n / ns;
+    for (uint64_t i = threadIdx.x; i < ns; i += TB) {
+        const int64_t d = delta[i * step];
+        if (d < 0) continue;
+        const uint64_t v = divide<DIV>((uint64_t)d, divisor);
+        uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
+        atomicAdd(&cnt[min(slot, nslots - 1)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t best = 0, bsum = 0;
+        for (uint32_t l = 0; l + W <= nslots; ++l) {
+            uint32_t sum = 0;
+            for (uint32_t j = 0; j < W; ++j) sum += cnt[l + j];
+            if (sum > bsum) { bsum = sum; best = l; }
+        }
+        *lo_out = best;
     }
 }
 
@@ -169,6 +228,8 @@ void launch(const HistArgs &a, uint32_t blocks, size_t lds, hipStream_t s, bool 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
         attr_set = true;
     }
+    if (a.lo) hipLaunchKernelGGL((k_hist_window<DIV>), dim3(1), dim3(TB), 0, s, a.delta, a.n, a.divisor, a.nslots,
+                                 a.W, const_cast<uint32_t *>(a.lo));
     if (vec) hipLaunchKernelGGL((k_hist<DIV, true>), dim3(blocks), dim3(TB), lds, s, a);
     else hipLaunchKernelGGL((k_hist<DIV, false>), dim3(blocks), dim3(TB), lds, s, a);
 }
@@ -205,10 +266,19 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
     a.ncont = ncont;
     a.nslots = nslots;
     const uint64_t nkeys = (uint64_t)a.ndev * ncont;
-    const uint64_t keys_fit = (LDS_BUDGET - 64) / (2ull * nslots);
+    a.W = nslots;
+    const uint64_t wfit = (LDS_BUDGET - 64) / (2ull * nkeys);   // slots per key for one partition
+    if (wfit < nslots && wfit >= 8 && !std::getenv("IGX_HIST_NOWINDOW")) {
+        a.W = (uint32_t)wfit;
+        void *sc;
+        int rc = igx_scratch(ctx, 256, &sc);
+        if (rc) return rc;
+        a.lo = static_cast<const uint32_t *>(sc);
+    }
+    const uint64_t keys_fit = (LDS_BUDGET - 64) / (2ull * a.W);
     a.P = (uint32_t)((nkeys + keys_fit - 1) / keys_fit);
     a.Kp = (uint32_t)((nkeys + a.P - 1) / a.P);
-    a.rep_words = (a.Kp * nslots + 1) / 2;
+    a.rep_words = (a.Kp * a.W + 1) / 2;
     const uint32_t part_bytes = a.rep_words * 4;
     a.R = std::max<uint32_t>(1, std::min<uint32_t>(TB / 64, LDS_BUDGET / part_bytes));
     // small histograms: keep two workgroups per CU

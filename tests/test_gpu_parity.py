@@ -178,6 +178,32 @@ def test_filter_c1(oracle, E, H, igx, torch):
     assert np.array_equal(H.host(srt["comm"]), ev_h["comm"][sel][perm])
 
 
+@pytest.mark.parametrize("spread", ["all-slots", "high-slots"])
+def test_hist_slot_window(oracle, E, H, torch, spread):
+    """4096 keys x 27 slots: LDS holds a window of the slots (k_hist header); rows outside
+    it go to HBM directly.  Deltas spread over every slot, or concentrated in high slots so
+    that the device-chosen window starts above 0."""
+    rng = np.random.default_rng(17 if spread == "all-slots" else 18)
+    n = 3_000_000
+    devs = [(8 << 20) | (16 * k) for k in range(16)]
+    dev = np.array(devs, np.uint32)[rng.integers(0, 16, n)]
+    cont = rng.integers(0, 256, n).astype(np.uint32)
+    if spread == "all-slots":
+        delta = (np.exp2(rng.uniform(0, 46, n)) * 1000).astype(np.int64)
+    else:
+        delta = (np.exp2(rng.normal(30, 1.5, n).clip(0, 60)) * 1000).astype(np.int64)
+    delta[::97] = -5                                              # negative: skipped
+    got = H.host(E.hist_log2(H.to_device(dev), H.to_device(cont), H.to_device(delta), devs, 256))
+    ref = oracle.hist_log2(dev, cont, delta, devs, 256)
+    assert np.array_equal(got, ref)
+    # one key, one in-window bin, far past the 16-bit LDS counters: window carries
+    d1 = torch.full((5_000_000,), 3 << 40, dtype=torch.int64, device="cuda")
+    dv = torch.full((5_000_000,), devs[5], dtype=torch.int32, device="cuda").view(torch.uint32)
+    cc = torch.full((5_000_000,), 200, dtype=torch.int32, device="cuda").view(torch.uint32)
+    h = H.host(E.hist_log2(dv, cc, d1, devs, 256))
+    assert int(h[5 * 256 + 200, 26]) == 5_000_000 and int(h.sum()) == 5_000_000
+
+
 def test_hist_log2_c3(oracle, E, H, torch):
     n = 2_000_000
     q = oracle.lognormal_quantiles(np.log(2e5), 1.5)
