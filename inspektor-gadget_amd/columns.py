@@ -173,29 +173,16 @@ class EventBatch:
 
     def take(self, idx):
         """Gather rows (device), keeping column dtypes."""
-        torch = torch_mod()
-        li = idx.to(torch.int64)
-        out = {k: gather(v, li) for k, v in self.data.items()}
-        valid = None if self.valid is None else self.valid.index_select(0, li)
+        from . import engine                 # igx_take on the device
+        names = list(self.data.keys())
+        ts = [self.data[k] for k in names] + ([] if self.valid is None else [self.valid])
+        outs = engine.take(ts, idx, self.n)
+        out = dict(zip(names, outs[:len(names)]))
+        valid = None if self.valid is None else outs[-1]
         return EventBatch(self.cols, out, valid)
 
     def to_host(self):
         return {k: host(v) for k, v in self.data.items()}
-
-
-_VIEW_AS = None
-
-
-def gather(t, li):
-    """index_select for every dtype (unsigned shell dtypes gather through a signed view)."""
-    torch = torch_mod()
-    global _VIEW_AS
-    if _VIEW_AS is None:
-        _VIEW_AS = {torch.uint16: torch.int16, torch.uint32: torch.int32, torch.uint64: torch.int64}
-    alt = _VIEW_AS.get(t.dtype)
-    if alt is not None:
-        return t.view(alt).index_select(0, li).view(t.dtype)
-    return t.index_select(0, li)
 
 
 def host(t):

@@ -124,3 +124,72 @@ int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }
+
+// ---- row gather (the compacted batch FilterEntries returns) ---------------------------------
+// One thread per (row, column): copies the row's width bytes in the widest unit that divides
+// the width and both base addresses.  Output rows are consecutive, so writes coalesce; reads
+// follow idx (ascending after a filter).  Indices >= nrows produce zero rows.
+namespace {
+
+constexpr uint32_t TAKE_MAXC = 16;
+
+struct TakeArgs {
+    const uint8_t *src[TAKE_MAXC];
+    uint8_t *dst[TAKE_MAXC];
+    uint32_t width[TAKE_MAXC];
+    uint32_t unit[TAKE_MAXC];
+};
+
+template <typename U>
+__device__ __forceinline__ void take_copy(const uint8_t *s, uint8_t *d, uint32_t width, bool ok) {
+    const U *su = reinterpret_cast<const U *>(s);
+    U *du = reinterpret_cast<U *>(d);
+    for (uint32_t w = 0; w < width / sizeof(U); ++w) du[w] = ok ? su[w] : U{};
+}
+
+__global__ __launch_bounds__(TB) void k_take(TakeArgs a, const uint32_t *__restrict__ idx, uint64_t k,
+                                             uint64_t nrows) {
+    const uint64_t r = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (r >= k) return;
+    const uint32_t c = blockIdx.y;
+    const uint32_t width = a.width[c];
+    const uint64_t g = idx[r];
+    const bool ok = g < nrows;
+    const uint8_t *s = a.src[c] + (ok ? g : 0) * width;
+    uint8_t *d = a.dst[c] + r * width;
+    switch (a.unit[c]) {
+    case 16: take_copy<uint4>(s, d, width, ok); break;
+    case 8: take_copy<uint64_t>(s, d, width, ok); break;
+    case 4: take_copy<uint32_t>(s, d, width, ok); break;
+    case 2: take_copy<uint16_t>(s, d, width, ok); break;
+    default: take_copy<uint8_t>(s, d, width, ok); break;
+    }
+}
+
+}  // namespace
+
+extern "C" int igx_take(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, uint64_t nrows,
+                        const uint32_t *idx, uint64_t k, void *const *out) {
+    if (!ctx) return IGX_EINVAL;
+    if (k == 0 || ncols == 0) return IGX_OK;
+    if (!cols || !idx || !out) return igx_fail(ctx, IGX_EINVAL, "take: null argument");
+    if (k >= (1ull << 32) * TB) return igx_fail(ctx, IGX_EINVAL, "take: too many rows");
+    for (uint32_t c0 = 0; c0 < ncols; c0 += TAKE_MAXC) {
+        const uint32_t nc = ncols - c0 < TAKE_MAXC ? ncols - c0 : TAKE_MAXC;
+        TakeArgs a{};
+        for (uint32_t j = 0; j < nc; ++j) {
+            const igx_col &col = cols[c0 + j];
+            if (!col.ptr || !out[c0 + j] || col.width == 0)
+                return igx_fail(ctx, IGX_EINVAL, "take: column %u has no data", c0 + j);
+            a.src[j] = static_cast<const uint8_t *>(col.ptr);
+            a.dst[j] = static_cast<uint8_t *>(out[c0 + j]);
+            a.width[j] = col.width;
+            const uint64_t al = (uint64_t)(uintptr_t)col.ptr | (uint64_t)(uintptr_t)out[c0 + j] | col.width;
+            a.unit[j] = (al & 15) == 0 ? 16 : (al & 7) == 0 ? 8 : (al & 3) == 0 ? 4 : (al & 1) == 0 ? 2 : 1;
+        }
+        hipLaunchKernelGGL(k_take, dim3((unsigned)((k + TB - 1) / TB), nc), dim3(TB), 0, ctx->stream, a, idx, k,
+                           nrows);
+    }
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}

@@ -142,4 +142,4 @@ def merge_topk(cand, key_bytes, naggs, sort_keys, k):
             for x, desc in sort_keys]
     first = allc[:, o + 8 * naggs:o + 8 * naggs + 8].contiguous().view(torch.uint64).flatten()
     idx = engine.sort_perm(keys, allc.shape[0], pos=first, k=k)
-    return allc.index_select(0, idx.view(torch.int32).to(torch.int64))
+    return engine.take([allc], idx)[0]

@@ -106,6 +106,27 @@ def filter_rows(cols, preds, n, valid=None):
     return out[:k]
 
 
+def take(tensors, idx, nrows=None):
+    """igx_take: rows idx (device u32/int32/int64) of every tensor ((n,) or (n, W)) gathered
+    on the device into fresh tensors of the same dtypes -- the compacted batch FilterEntries
+    returns (filter.go:294-325)."""
+    torch = torch_mod()
+    ctx = context()
+    if idx.dtype not in (torch.int32, torch.uint32):
+        idx = idx.to(torch.int32)
+    idx = idx.contiguous()
+    k = int(idx.numel())
+    tensors = [t.contiguous() for t in tensors]
+    outs = [torch.empty((k,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors]
+    if k and tensors:
+        n = int(tensors[0].shape[0]) if nrows is None else nrows
+        ccols = (Col * len(tensors))(*[col_of(t, dtype_kind(t), t[0].numel() * t.element_size() if t.dim() > 1 else None)
+                                         for t in tensors])
+        dst = (C.c_void_p * len(outs))(*[o.data_ptr() for o in outs])
+        ctx.check(ctx.L.igx_take(ctx.h, ccols, len(tensors), n, ptr(idx), k, dst))
+    return outs
+
+
 # ------------------------------------------------------------------------------------
 # sort
 # ------------------------------------------------------------------------------------

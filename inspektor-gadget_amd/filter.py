@@ -89,7 +89,7 @@ def _scan(batch: EventBatch, specs):
         else:
             sub = batch.take(idx)
             sel = engine.filter_rows(sub.tensors_in_schema_order(), preds, sub.n, sub.valid)
-            idx = idx.view(torch.int32).index_select(0, sel.to(torch.int64)).view(torch.uint32)
+            idx = engine.take([idx], sel)[0]
     return idx
 
 

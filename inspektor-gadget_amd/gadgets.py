@@ -183,7 +183,7 @@ class _TopTracer:
             t = self.batches[j][2].get(name)
             if t is None:
                 continue
-            li = torch.tensor([r for _, r in lst], dtype=torch.int64, device=t.device)
+            li = torch.tensor([r for _, r in lst], dtype=torch.int32, device=t.device)
             vals = host(_take(t, li))
             for (i, _), v in zip(lst, vals):
                 out[i] = v
@@ -228,8 +228,8 @@ class _TopTracer:
 
 
 def _take(t, li):
-    from .columns import gather
-    return gather(t, li)
+    from . import engine                     # igx_take on the device
+    return engine.take([t], li)[0]
 
 
 def _stats_columns(fields, extractors=(), virtual=()):

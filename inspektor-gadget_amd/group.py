@@ -18,7 +18,7 @@ from __future__ import annotations
 
 from . import _abi
 from ._abi import IgxError
-from .columns import Columns, EventBatch, GroupTypeSum, KINDS, gather
+from .columns import Columns, EventBatch, GroupTypeSum, KINDS
 from .runtime import torch_mod
 from . import engine
 

@@ -178,6 +178,33 @@ def test_filter_c1(oracle, E, H, igx, torch):
     assert np.array_equal(H.host(srt["comm"]), ev_h["comm"][sel][perm])
 
 
+def test_take_rows(E, H, torch):
+    """igx_take (the compacted batch FilterEntries returns): every width / alignment unit,
+    more than one launch's worth of columns, out-of-range indices -> zero rows, empty idx."""
+    rng = np.random.default_rng(7)
+    n, k = 100_003, 70_001
+    specs = [(np.uint8, None), (np.uint16, None), (np.uint32, None), (np.uint64, None),
+             (np.int64, None), (np.uint8, 16), (np.uint8, 3), (np.uint8, 24), (np.uint8, 72)] * 2
+    cols = []
+    for dt, w in specs:
+        shape = (n,) if w is None else (n, w)
+        cols.append(rng.integers(0, 256 if w else np.iinfo(dt).max, size=shape, dtype=dt))
+    idx = rng.integers(0, n, size=k).astype(np.uint32)
+    idx[::997] = n + 5                                   # out of range -> zero row
+    got = E.take([H.to_device(c) for c in cols], H.to_device(idx), n)
+    ok = idx < n
+    for c, g in zip(cols, got):
+        want = np.zeros((k,) + c.shape[1:], dtype=c.dtype)
+        want[ok] = c[idx[ok]]
+        assert np.array_equal(H.host(g), want), (c.dtype, c.shape)
+    # a byte column whose base address is odd (contiguous, storage offset 5)
+    flat = rng.integers(0, 256, size=n * 24 + 5, dtype=np.uint8)
+    sub = H.to_device(flat)[5:].view(n, 24)
+    got = E.take([sub], H.to_device(idx[ok]), n)[0]
+    assert np.array_equal(H.host(got), flat[5:].reshape(n, 24)[idx[ok]])
+    assert E.take([H.to_device(cols[0])], H.to_device(np.zeros(0, np.uint32)), n)[0].numel() == 0
+
+
 @pytest.mark.parametrize("spread", ["all-slots", "high-slots"])
 def test_hist_slot_window(oracle, E, H, torch, spread):
     """4096 keys x 27 slots: LDS holds a window of the slots (k_hist header); rows outside

@@ -61,8 +61,7 @@ def c1(igx, O, torch, reps):
 
     def run():
         idx = E.filter_rows(tcols, preds, n)
-        li = idx.to(torch.int64)
-        comm, pid = ev["comm"].index_select(0, li), ev["pid"].index_select(0, li)
+        comm, pid = E.take([ev["comm"], ev["pid"]], idx, n)
         state["perm"] = E.sort_perm([(comm, False), (pid, True)], idx.numel())
         state["idx"] = idx
     ms = timed(torch, run, reps)
