@@ -107,5 +107,5 @@ def FilterEntries(cols: Columns, batch, filters):
         out = out.take(idx)
     if not filters:
         # no filters: the reference returns its (nil) outEntries slice
-        return batch.take(batch.valid.nonzero().flatten()) if batch.valid is not None else batch
+        return batch.take(_scan(batch, [])) if batch.valid is not None else batch   # drops nil rows
     return out

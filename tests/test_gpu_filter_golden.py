@@ -69,3 +69,26 @@ def test_filter_table_multi_on_device(igx):
     d, cols, batch = _device_fixture(igx)
     sel = H.host(F.GetFiltersFromStrings(cols, d["multi"]["filters"]).MatchAll(batch))
     assert len(sel) == 1
+
+
+def test_filter_entries_nil_rows_and_chaining(igx):
+    """FilterEntries (filter.go:294-325) over the golden records + nil: no filters keeps the
+    non-nil rows in order; each filter compacts the batch (igx_take) before the next one;
+    more than 4 predicates in one MatchAll chain through the compacted ids."""
+    F, H = igx.filter, igx.columns
+    d, cols, batch = _device_fixture(igx)
+    recs = d["records"]
+    live = [i for i, r in enumerate(recs) if r is not None]
+    out = F.FilterEntries(cols, batch, [])
+    assert out.n == len(live)
+    assert np.array_equal(H.host(out.valid), np.ones(len(live), np.uint8))
+    name = next(n for n, k in d["columns"] if k == "string")
+    assert np.array_equal(H.host(out[name]), H.host(batch[name])[live])
+    rows = [r for r in d["rows"] if not r["error"] and r["count"] > 0]
+    # the same filter five times: MatchAll takes 4 per scan, the fifth chains via igx_take
+    f = rows[0]["filter"]
+    sel = H.host(F.GetFiltersFromStrings(cols, [f] * 5).MatchAll(batch))
+    assert len(sel) == rows[0]["count"]
+    assert np.array_equal(sel, H.host(F.GetFiltersFromStrings(cols, [f]).MatchAll(batch)))
+    chained = F.FilterEntries(cols, batch, [f, f])
+    assert chained.n == rows[0]["count"]
