@@ -157,6 +157,11 @@ int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t
 int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
                uint64_t *out_n);
+/* FilterSpecs.MatchAny (filter.go:276-283): OR of preds (any number), nil rows never match,
+ * zero preds select nothing.  Outputs as igx_filter.  Asynchronous. */
+int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                   uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                   uint64_t *out_n);
 /* The compacted batch FilterEntries returns (filter.go:294-325 builds a fresh slice of the
  * selected entries): rows idx[0..k) (device u32, e.g. igx_filter's out_idx) of every column
  * gathered into out[c] (device, k * cols[c].width bytes, rows packed).  Indices >= nrows

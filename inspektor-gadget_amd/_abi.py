@@ -100,6 +100,7 @@ SIGNATURES = [
                               C.c_char_p, _SZ]),
     ("igx_regex_compile_blob", _I, [C.c_char_p, _SZ, _VP, _SZ, C.POINTER(_SZ), C.c_char_p, _SZ]),
     ("igx_filter", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _VP, _VP]),
+    ("igx_filter_any", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _VP, _VP]),
     ("igx_take", _I, [_VP, C.POINTER(Col), _U32, _U64, _VP, _U64, C.POINTER(_VP)]),
     ("igx_sort_prepare", _I, [C.POINTER(SchemaCol), _U32, C.POINTER(C.c_char_p), _U32,
                               C.POINTER(SortKey), C.POINTER(_U32), C.POINTER(_U32)]),

@@ -489,6 +489,24 @@ extern "C" int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, con
     return launch_filter(ctx, dp, valid, nrows, out_idx, out_n);
 }
 
+extern "C" int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                              uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                              uint64_t *out_n) {
+    if (!ctx) return IGX_EINVAL;
+    if (!out_n || (nrows && !out_idx)) return igx_fail(ctx, IGX_EINVAL, "filter: null output");
+    if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "filter: more than 2^32 rows");
+    if (npreds && !preds) return igx_fail(ctx, IGX_EINVAL, "filter: null predicates");
+    const uint32_t nchunks = npreds ? (npreds + IGX_KMAX_PREDS - 1) / IGX_KMAX_PREDS : 1;
+    std::vector<DevPreds> dps(nchunks);
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t b = c * IGX_KMAX_PREDS;
+        const uint32_t m = npreds - b < IGX_KMAX_PREDS ? npreds - b : IGX_KMAX_PREDS;
+        int rc = igx_build_preds(ctx, cols, ncols, npreds ? preds + b : nullptr, npreds ? m : 0, &dps[c]);
+        if (rc) return rc;
+    }
+    return launch_filter_chunks(ctx, dps.data(), nchunks, 1, valid, nrows, out_idx, out_n);
+}
+
 // ---------------------------------------------------------------------------------------
 // sort
 // ---------------------------------------------------------------------------------------

@@ -176,6 +176,13 @@ __device__ __forceinline__ bool preds_match_all(const DevPreds &dp, uint64_t row
     return ok;
 }
 
+// FilterSpecs.MatchAny (filter.go:276-283): true on the first matching spec
+__device__ __forceinline__ bool preds_match_any(const DevPreds &dp, uint64_t row) {
+    bool ok = false;
+    for (uint32_t p = 0; p < dp.n; ++p) ok = ok || pred_match(dp.p[p], row);
+    return ok;
+}
+
 // agent-scope relaxed loads/stores: `global_load/store ... sc1` on gfx950 -- the
 // write-through / L1-bypass forms MI355X_MICROARCH.md §Workgroup dispatch validates
 // for cross-workgroup hand-offs.

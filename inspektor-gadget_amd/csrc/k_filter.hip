@@ -19,9 +19,13 @@ constexpr int RPT = 4;             // rows per thread per tile
 constexpr int TILE = TB * RPT;     // 1024 rows per tile
 constexpr int WPT = TILE / 64;     // mask words per tile
 
+// any = 0: AND of dp's predicates (MatchAll); any = 1: OR (MatchAny).  acc = 1 ORs the
+// tile's bits into the mask an earlier launch wrote (MatchAny over more than
+// IGX_KMAX_PREDS specs); the counts are always those of the combined mask.
 __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *__restrict__ valid,
                                                     uint64_t n, uint64_t *__restrict__ mask,
-                                                    uint32_t *__restrict__ tile_cnt) {
+                                                    uint32_t *__restrict__ tile_cnt, uint32_t any,
+                                                    uint32_t acc) {
     __shared__ uint32_t wcnt[TB / 64];
     const uint64_t tile = blockIdx.x;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -31,9 +35,10 @@ __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *
         uint64_t row = tile * TILE + (uint64_t)j * TB + threadIdx.x;
         bool ok = row < n;
         if (ok && valid) ok = valid[row] != 0;
-        if (ok) ok = preds_match_all(dp, row);
+        if (ok) ok = any ? preds_match_any(dp, row) : preds_match_all(dp, row);
         uint64_t b = __ballot(ok);
         if (lane == 0) {
+            if (acc) b |= mask[tile * WPT + j * (TB / 64) + wave];
             mask[tile * WPT + j * (TB / 64) + wave] = b;
             cnt += __popcll(b);
         }
@@ -102,6 +107,11 @@ __global__ __launch_bounds__(TB) void k_filter_compact(const uint64_t *__restric
 
 int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64_t nrows,
                   uint32_t *out_idx, uint64_t *out_n) {
+    return launch_filter_chunks(ctx, &dp, 1, 0, valid, nrows, out_idx, out_n);
+}
+
+int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, uint32_t any,
+                         const uint8_t *valid, uint64_t nrows, uint32_t *out_idx, uint64_t *out_n) {
     if (nrows == 0) {
         IGX_HIP(ctx, hipMemsetAsync(out_n, 0, sizeof(uint64_t), ctx->stream));
         return IGX_OK;
@@ -116,8 +126,9 @@ int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64
     auto *mask = reinterpret_cast<uint64_t *>(s);
     auto *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s) + mask_b);
     auto *off = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(s) + mask_b + cnt_b);
-    hipLaunchKernelGGL(k_filter_mark, dim3(ntiles), dim3(TB), 0, ctx->stream, dp, valid, nrows,
-                       mask, cnt);
+    for (uint32_t c = 0; c < nchunks; ++c)
+        hipLaunchKernelGGL(k_filter_mark, dim3(ntiles), dim3(TB), 0, ctx->stream, dps[c], valid, nrows,
+                           mask, cnt, any, c > 0 ? 1u : 0u);
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, ctx->stream, cnt, ntiles, off, out_n);
     hipLaunchKernelGGL(k_filter_compact, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, off, nrows,
                        out_idx);

@@ -90,8 +90,9 @@ def gen_file(seed, rank, G, cdf, base, n):
 # ------------------------------------------------------------------------------------
 # filter
 # ------------------------------------------------------------------------------------
-def filter_rows(cols, preds, n, valid=None):
+def filter_rows(cols, preds, n, valid=None, any=False):
     """cols: list of device tensors (indexed by Pred.col); preds: list of Pred.
+    any=False: igx_filter (AND, at most 4 preds); any=True: igx_filter_any (OR, any number).
     Returns (idx u32 tensor of length n_selected)."""
     torch = torch_mod()
     ctx = context()
@@ -100,8 +101,8 @@ def filter_rows(cols, preds, n, valid=None):
     cpreds = (Pred * max(1, len(preds)))(*preds)
     out = torch.empty(max(1, n), dtype=torch.uint32, device=dev)
     cnt = torch.zeros(1, dtype=torch.uint64, device=dev)
-    ctx.check(ctx.L.igx_filter(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n,
-                               ptr(out), ptr(cnt)))
+    fn = ctx.L.igx_filter_any if any else ctx.L.igx_filter
+    ctx.check(fn(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n, ptr(out), ptr(cnt)))
     k = int(cnt.item())
     return out[:k]
 

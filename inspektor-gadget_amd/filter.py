@@ -48,11 +48,8 @@ class FilterSpecs(list):
         torch = torch_mod()
         if not self:
             return torch.empty(0, dtype=torch.uint32, device=batch.device())
-        mark = torch.zeros(batch.n, dtype=torch.bool, device=batch.device())
-        for fs in self:
-            idx = _scan(batch, [fs])
-            mark[idx.to(torch.int64)] = True
-        return torch.nonzero(mark).flatten().to(torch.int32).view(torch.uint32)
+        return engine.filter_rows(batch.tensors_in_schema_order(), [s.pred for s in self],
+                                  batch.n, batch.valid, any=True)
 
 
 def GetFilterFromString(cols: Columns, filt: str) -> FilterSpec:

@@ -92,3 +92,21 @@ def test_filter_entries_nil_rows_and_chaining(igx):
     assert np.array_equal(sel, H.host(F.GetFiltersFromStrings(cols, [f]).MatchAll(batch)))
     chained = F.FilterEntries(cols, batch, [f, f])
     assert chained.n == rows[0]["count"]
+
+
+def test_match_any_on_device(igx):
+    """FilterSpecs.MatchAny (filter.go:276-283) through igx_filter_any: the union of the
+    single-filter selections of the golden table, for 1, 4 and 9 specs (more than one
+    predicate chunk), nil never matching; no specs select nothing."""
+    F, H = igx.filter, igx.columns
+    d, cols, batch = _device_fixture(igx)
+    good = [r["filter"] for r in d["rows"] if not r["error"]]
+    rng = np.random.default_rng(3)
+    for m in (1, 4, 9, 9, 9):
+        pick = [good[i] for i in rng.choice(len(good), size=m, replace=False)]
+        union = set()
+        for f in pick:
+            union |= set(H.host(F.GetFiltersFromStrings(cols, [f]).MatchAll(batch)).tolist())
+        got = H.host(F.GetFiltersFromStrings(cols, pick).MatchAny(batch))
+        assert got.tolist() == sorted(union), pick
+    assert F.FilterSpecs().MatchAny(batch).numel() == 0
