@@ -151,7 +151,7 @@ int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *fil
 int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
                            size_t *out_len, char *errbuf, size_t errlen);
 
-/* FilterEntries / MatchAll: AND of preds over rows [0,nrows), order-preserving.
+/* FilterEntries / MatchAll: AND of preds (any number) over rows [0,nrows), order-preserving.
  * valid (device, nullable): 0 marks a nil entry (skipped).  out_idx (device) receives
  * the selected row ids; *out_n (device u64) their count.  Asynchronous. */
 int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,

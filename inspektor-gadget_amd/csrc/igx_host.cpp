@@ -477,21 +477,9 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
     return IGX_OK;
 }
 
-extern "C" int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
-                          uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
-                          uint64_t *out_n) {
-    if (!ctx) return IGX_EINVAL;
-    if (!out_n || (nrows && !out_idx)) return igx_fail(ctx, IGX_EINVAL, "filter: null output");
-    if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "filter: more than 2^32 rows");
-    DevPreds dp;
-    int rc = igx_build_preds(ctx, cols, ncols, preds, npreds, &dp);
-    if (rc) return rc;
-    return launch_filter(ctx, dp, valid, nrows, out_idx, out_n);
-}
-
-extern "C" int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
-                              uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
-                              uint64_t *out_n) {
+static int filter_chunked(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                          uint32_t npreds, uint32_t any, const uint8_t *valid, uint64_t nrows,
+                          uint32_t *out_idx, uint64_t *out_n) {
     if (!ctx) return IGX_EINVAL;
     if (!out_n || (nrows && !out_idx)) return igx_fail(ctx, IGX_EINVAL, "filter: null output");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "filter: more than 2^32 rows");
@@ -504,7 +492,19 @@ extern "C" int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols,
         int rc = igx_build_preds(ctx, cols, ncols, npreds ? preds + b : nullptr, npreds ? m : 0, &dps[c]);
         if (rc) return rc;
     }
-    return launch_filter_chunks(ctx, dps.data(), nchunks, 1, valid, nrows, out_idx, out_n);
+    return launch_filter_chunks(ctx, dps.data(), nchunks, any, valid, nrows, out_idx, out_n);
+}
+
+extern "C" int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                          uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                          uint64_t *out_n) {
+    return filter_chunked(ctx, cols, ncols, preds, npreds, 0, valid, nrows, out_idx, out_n);
+}
+
+extern "C" int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                              uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                              uint64_t *out_n) {
+    return filter_chunked(ctx, cols, ncols, preds, npreds, 1, valid, nrows, out_idx, out_n);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -19,9 +19,9 @@ constexpr int RPT = 4;             // rows per thread per tile
 constexpr int TILE = TB * RPT;     // 1024 rows per tile
 constexpr int WPT = TILE / 64;     // mask words per tile
 
-// any = 0: AND of dp's predicates (MatchAll); any = 1: OR (MatchAny).  acc = 1 ORs the
-// tile's bits into the mask an earlier launch wrote (MatchAny over more than
-// IGX_KMAX_PREDS specs); the counts are always those of the combined mask.
+// any = 0: AND of dp's predicates (MatchAll); any = 1: OR (MatchAny).  acc = 1 combines the
+// tile's bits (AND / OR) with the mask an earlier launch wrote (more than IGX_KMAX_PREDS
+// specs); the counts are always those of the combined mask.
 __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *__restrict__ valid,
                                                     uint64_t n, uint64_t *__restrict__ mask,
                                                     uint32_t *__restrict__ tile_cnt, uint32_t any,
@@ -38,7 +38,10 @@ __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *
         if (ok) ok = any ? preds_match_any(dp, row) : preds_match_all(dp, row);
         uint64_t b = __ballot(ok);
         if (lane == 0) {
-            if (acc) b |= mask[tile * WPT + j * (TB / 64) + wave];
+            if (acc) {
+                const uint64_t prev = mask[tile * WPT + j * (TB / 64) + wave];
+                b = any ? (b | prev) : (b & prev);
+            }
             mask[tile * WPT + j * (TB / 64) + wave] = b;
             cnt += __popcll(b);
         }

@@ -92,7 +92,7 @@ def gen_file(seed, rank, G, cdf, base, n):
 # ------------------------------------------------------------------------------------
 def filter_rows(cols, preds, n, valid=None, any=False):
     """cols: list of device tensors (indexed by Pred.col); preds: list of Pred.
-    any=False: igx_filter (AND, at most 4 preds); any=True: igx_filter_any (OR, any number).
+    any=False: igx_filter (AND); any=True: igx_filter_any (OR); any number of preds.
     Returns (idx u32 tensor of length n_selected)."""
     torch = torch_mod()
     ctx = context()

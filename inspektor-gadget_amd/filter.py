@@ -75,19 +75,10 @@ def GetFiltersFromStrings(cols: Columns, filters) -> FilterSpecs:
 
 
 def _scan(batch: EventBatch, specs):
-    """AND of specs over the batch on the device; returns selected row ids (u32)."""
-    torch = torch_mod()
-    tensors = batch.tensors_in_schema_order()
-    for i in range(0, max(1, len(specs)), 4):      # kernel takes up to 4 predicates
-        chunk = specs[i:i + 4]
-        preds = [s.pred for s in chunk]
-        if i == 0:
-            idx = engine.filter_rows(tensors, preds, batch.n, batch.valid)
-        else:
-            sub = batch.take(idx)
-            sel = engine.filter_rows(sub.tensors_in_schema_order(), preds, sub.n, sub.valid)
-            idx = engine.take([idx], sel)[0]
-    return idx
+    """AND of specs over the batch on the device (igx_filter: 4 predicates per mark launch,
+    later launches AND into the same bitmask); returns selected row ids (u32)."""
+    return engine.filter_rows(batch.tensors_in_schema_order(), [s.pred for s in specs],
+                              batch.n, batch.valid)
 
 
 def FilterEntries(cols: Columns, batch, filters):

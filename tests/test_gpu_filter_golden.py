@@ -74,7 +74,7 @@ def test_filter_table_multi_on_device(igx):
 def test_filter_entries_nil_rows_and_chaining(igx):
     """FilterEntries (filter.go:294-325) over the golden records + nil: no filters keeps the
     non-nil rows in order; each filter compacts the batch (igx_take) before the next one;
-    more than 4 predicates in one MatchAll chain through the compacted ids."""
+    more than 4 predicates in one MatchAll AND into one bitmask over several mark launches."""
     F, H = igx.filter, igx.columns
     d, cols, batch = _device_fixture(igx)
     recs = d["records"]
@@ -85,7 +85,7 @@ def test_filter_entries_nil_rows_and_chaining(igx):
     name = next(n for n, k in d["columns"] if k == "string")
     assert np.array_equal(H.host(out[name]), H.host(batch[name])[live])
     rows = [r for r in d["rows"] if not r["error"] and r["count"] > 0]
-    # the same filter five times: MatchAll takes 4 per scan, the fifth chains via igx_take
+    # the same filter five times: 4 predicates per mark launch, the fifth ANDs into the mask
     f = rows[0]["filter"]
     sel = H.host(F.GetFiltersFromStrings(cols, [f] * 5).MatchAll(batch))
     assert len(sel) == rows[0]["count"]
@@ -95,9 +95,10 @@ def test_filter_entries_nil_rows_and_chaining(igx):
 
 
 def test_match_any_on_device(igx):
-    """FilterSpecs.MatchAny (filter.go:276-283) through igx_filter_any: the union of the
-    single-filter selections of the golden table, for 1, 4 and 9 specs (more than one
-    predicate chunk), nil never matching; no specs select nothing."""
+    """FilterSpecs.MatchAny (filter.go:276-283) through igx_filter_any and MatchAll
+    (:266-273) through igx_filter: the union / intersection of the single-filter selections
+    of the golden table, for 1, 4 and 9 specs (more than one predicate chunk), nil never
+    matching; no specs select nothing."""
     F, H = igx.filter, igx.columns
     d, cols, batch = _device_fixture(igx)
     good = [r["filter"] for r in d["rows"] if not r["error"]]
@@ -109,4 +110,9 @@ def test_match_any_on_device(igx):
             union |= set(H.host(F.GetFiltersFromStrings(cols, [f]).MatchAll(batch)).tolist())
         got = H.host(F.GetFiltersFromStrings(cols, pick).MatchAny(batch))
         assert got.tolist() == sorted(union), pick
+        inter = set(range(len(d["records"])))
+        for f in pick:
+            inter &= set(H.host(F.GetFiltersFromStrings(cols, [f]).MatchAll(batch)).tolist())
+        got = H.host(F.GetFiltersFromStrings(cols, pick).MatchAll(batch))
+        assert got.tolist() == sorted(inter), pick
     assert F.FilterSpecs().MatchAny(batch).numel() == 0
