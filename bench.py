@@ -202,7 +202,7 @@ def merge_candidates(E, H, allc, K):
     recv = allc[:, 80:88].contiguous().view(torch.uint64).flatten()
     first = allc[:, 88:96].contiguous().view(torch.uint64).flatten()
     idx = E.sort_perm([(sent, True), (recv, True)], allc.shape[0], pos=first, k=K)
-    return allc.index_select(0, idx.view(torch.int32).to(torch.int64))
+    return E.take([allc], idx)[0]
 
 
 def verify(O, cdf_h, G, N, K, cand, H):
