@@ -151,17 +151,32 @@ int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *fil
 int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
                            size_t *out_len, char *errbuf, size_t errlen);
 
-/* FilterEntries / MatchAll: AND of preds (any number) over rows [0,nrows), order-preserving.
- * valid (device, nullable): 0 marks a nil entry (skipped).  out_idx (device) receives
- * the selected row ids; *out_n (device u64) their count.  Asynchronous. */
+/* FilterEntries' per-filter pass (filter.go:301-322): AND of preds (any number) over rows
+ * [0,nrows), order-preserving.  valid (device, nullable): 0 marks a nil entry, which is
+ * skipped (:310-314).  out_idx (device) receives the selected row ids; *out_n (device u64)
+ * their count.  Asynchronous. */
 int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
                uint64_t *out_n);
-/* FilterSpecs.MatchAny (filter.go:276-283): OR of preds (any number), nil rows never match,
- * zero preds select nothing.  Outputs as igx_filter.  Asynchronous. */
+/* FilterSpecs.MatchAny (filter.go:276-283): OR of preds (any number); zero preds select
+ * nothing; a nil row matches iff some pred is negated (Match(nil) == negate, :286-291).
+ * Outputs as igx_filter.  Asynchronous. */
 int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                    uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
                    uint64_t *out_n);
+/* The general form.  flags:
+ *   IGX_FILTER_ANY        OR of preds (MatchAny) instead of AND (MatchAll);
+ *   IGX_FILTER_NIL_MATCH  a nil row yields Match(nil) == negate for every pred (filter.go:
+ *                         286-291), combined like the other rows: FilterSpecs.MatchAll keeps a
+ *                         nil row iff every pred is negated (or there are none), MatchAny iff
+ *                         one is -- what parser.eventHandlerArray relies on (parser.go:209-218).
+ *                         Without it nil rows are skipped (FilterEntries).
+ * igx_filter == flags 0; igx_filter_any == IGX_FILTER_ANY | IGX_FILTER_NIL_MATCH. */
+#define IGX_FILTER_ANY 1u
+#define IGX_FILTER_NIL_MATCH 2u
+int igx_filter_ex(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                  uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t flags,
+                  uint32_t *out_idx, uint64_t *out_n);
 /* The compacted batch FilterEntries returns (filter.go:294-325 builds a fresh slice of the
  * selected entries): rows idx[0..k) (device u32, e.g. igx_filter's out_idx) of every column
  * gathered into out[c] (device, k * cols[c].width bytes, rows packed).  Indices >= nrows

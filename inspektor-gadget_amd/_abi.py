@@ -23,6 +23,7 @@ COL_VIRTUAL, COL_EXTRACTOR = 1, 2
 NO_COL = 0xFFFFFFFF
 MAX_REF = 256
 AGG_COUNT, AGG_SUM = 0, 1
+FILTER_ANY, FILTER_NIL_MATCH = 1, 2
 
 
 class SchemaCol(C.Structure):
@@ -101,6 +102,8 @@ SIGNATURES = [
     ("igx_regex_compile_blob", _I, [C.c_char_p, _SZ, _VP, _SZ, C.POINTER(_SZ), C.c_char_p, _SZ]),
     ("igx_filter", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _VP, _VP]),
     ("igx_filter_any", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _VP, _VP]),
+    ("igx_filter_ex", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(Pred), _U32, _VP, _U64, _U32, _VP,
+                           _VP]),
     ("igx_take", _I, [_VP, C.POINTER(Col), _U32, _U64, _VP, _U64, C.POINTER(_VP)]),
     ("igx_sort_prepare", _I, [C.POINTER(SchemaCol), _U32, C.POINTER(C.c_char_p), _U32,
                               C.POINTER(SortKey), C.POINTER(_U32), C.POINTER(_U32)]),

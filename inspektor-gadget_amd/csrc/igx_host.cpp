@@ -478,9 +478,11 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
 }
 
 static int filter_chunked(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
-                          uint32_t npreds, uint32_t any, const uint8_t *valid, uint64_t nrows,
+                          uint32_t npreds, uint32_t flags, const uint8_t *valid, uint64_t nrows,
                           uint32_t *out_idx, uint64_t *out_n) {
     if (!ctx) return IGX_EINVAL;
+    if (flags & ~(uint32_t)(IGX_FILTER_ANY | IGX_FILTER_NIL_MATCH))
+        return igx_fail(ctx, IGX_EINVAL, "filter: unknown flags 0x%x", flags);
     if (!out_n || (nrows && !out_idx)) return igx_fail(ctx, IGX_EINVAL, "filter: null output");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "filter: more than 2^32 rows");
     if (npreds && !preds) return igx_fail(ctx, IGX_EINVAL, "filter: null predicates");
@@ -492,7 +494,8 @@ static int filter_chunked(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, con
         int rc = igx_build_preds(ctx, cols, ncols, npreds ? preds + b : nullptr, npreds ? m : 0, &dps[c]);
         if (rc) return rc;
     }
-    return launch_filter_chunks(ctx, dps.data(), nchunks, any, valid, nrows, out_idx, out_n);
+    return launch_filter_chunks(ctx, dps.data(), nchunks, (flags & IGX_FILTER_ANY) ? 1u : 0u,
+                                (flags & IGX_FILTER_NIL_MATCH) ? 1u : 0u, valid, nrows, out_idx, out_n);
 }
 
 extern "C" int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
@@ -504,7 +507,14 @@ extern "C" int igx_filter(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, con
 extern "C" int igx_filter_any(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                               uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
                               uint64_t *out_n) {
-    return filter_chunked(ctx, cols, ncols, preds, npreds, 1, valid, nrows, out_idx, out_n);
+    return filter_chunked(ctx, cols, ncols, preds, npreds, IGX_FILTER_ANY | IGX_FILTER_NIL_MATCH, valid, nrows,
+                          out_idx, out_n);
+}
+
+extern "C" int igx_filter_ex(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
+                             uint32_t npreds, const uint8_t *valid, uint64_t nrows, uint32_t flags,
+                             uint32_t *out_idx, uint64_t *out_n) {
+    return filter_chunked(ctx, cols, ncols, preds, npreds, flags, valid, nrows, out_idx, out_n);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -68,7 +68,8 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
 int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64_t nrows,
                   uint32_t *out_idx, uint64_t *out_n);
 int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, uint32_t any,
-                         const uint8_t *valid, uint64_t nrows, uint32_t *out_idx, uint64_t *out_n);
+                         uint32_t nil_match, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                         uint64_t *out_n);
 
 struct SortPlanKey {
     const uint8_t *ptr;

@@ -21,11 +21,14 @@ constexpr int WPT = TILE / 64;     // mask words per tile
 
 // any = 0: AND of dp's predicates (MatchAll); any = 1: OR (MatchAny).  acc = 1 combines the
 // tile's bits (AND / OR) with the mask an earlier launch wrote (more than IGX_KMAX_PREDS
-// specs); the counts are always those of the combined mask.
+// specs); the counts are always those of the combined mask.  nil_bit is what a nil row
+// (valid == 0) yields for this chunk: 0 for FilterEntries, which skips nil entries
+// (filter.go:310-314); the AND (MatchAll) or OR (MatchAny) of the chunk's negate flags for
+// FilterSpecs.Match(nil) == negate (filter.go:286-291).
 __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *__restrict__ valid,
                                                     uint64_t n, uint64_t *__restrict__ mask,
                                                     uint32_t *__restrict__ tile_cnt, uint32_t any,
-                                                    uint32_t acc) {
+                                                    uint32_t acc, uint32_t nil_bit) {
     __shared__ uint32_t wcnt[TB / 64];
     const uint64_t tile = blockIdx.x;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -34,8 +37,8 @@ __global__ __launch_bounds__(TB) void k_filter_mark(DevPreds dp, const uint8_t *
     for (int j = 0; j < RPT; ++j) {
         uint64_t row = tile * TILE + (uint64_t)j * TB + threadIdx.x;
         bool ok = row < n;
-        if (ok && valid) ok = valid[row] != 0;
-        if (ok) ok = any ? preds_match_any(dp, row) : preds_match_all(dp, row);
+        if (ok && valid && valid[row] == 0) ok = nil_bit != 0;
+        else if (ok) ok = any ? preds_match_any(dp, row) : preds_match_all(dp, row);
         uint64_t b = __ballot(ok);
         if (lane == 0) {
             if (acc) {
@@ -110,11 +113,12 @@ __global__ __launch_bounds__(TB) void k_filter_compact(const uint64_t *__restric
 
 int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64_t nrows,
                   uint32_t *out_idx, uint64_t *out_n) {
-    return launch_filter_chunks(ctx, &dp, 1, 0, valid, nrows, out_idx, out_n);
+    return launch_filter_chunks(ctx, &dp, 1, 0, 0, valid, nrows, out_idx, out_n);
 }
 
 int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, uint32_t any,
-                         const uint8_t *valid, uint64_t nrows, uint32_t *out_idx, uint64_t *out_n) {
+                         uint32_t nil_match, const uint8_t *valid, uint64_t nrows, uint32_t *out_idx,
+                         uint64_t *out_n) {
     if (nrows == 0) {
         IGX_HIP(ctx, hipMemsetAsync(out_n, 0, sizeof(uint64_t), ctx->stream));
         return IGX_OK;
@@ -129,9 +133,15 @@ int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, ui
     auto *mask = reinterpret_cast<uint64_t *>(s);
     auto *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s) + mask_b);
     auto *off = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(s) + mask_b + cnt_b);
-    for (uint32_t c = 0; c < nchunks; ++c)
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        // Match(nil) == negate, combined over the chunk like the predicates themselves
+        uint32_t nil_bit = any ? 0u : 1u;
+        for (uint32_t p = 0; p < dps[c].n; ++p)
+            nil_bit = any ? (nil_bit | (dps[c].p[p].negate != 0)) : (nil_bit & (dps[c].p[p].negate != 0));
+        if (!nil_match) nil_bit = 0;
         hipLaunchKernelGGL(k_filter_mark, dim3(ntiles), dim3(TB), 0, ctx->stream, dps[c], valid, nrows,
-                           mask, cnt, any, c > 0 ? 1u : 0u);
+                           mask, cnt, any, c > 0 ? 1u : 0u, nil_bit);
+    }
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, ctx->stream, cnt, ntiles, off, out_n);
     hipLaunchKernelGGL(k_filter_compact, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, off, nrows,
                        out_idx);

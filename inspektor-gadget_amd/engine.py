@@ -90,19 +90,22 @@ def gen_file(seed, rank, G, cdf, base, n):
 # ------------------------------------------------------------------------------------
 # filter
 # ------------------------------------------------------------------------------------
-def filter_rows(cols, preds, n, valid=None, any=False):
+def filter_rows(cols, preds, n, valid=None, any=False, nil_match=False):
     """cols: list of device tensors (indexed by Pred.col); preds: list of Pred.
-    any=False: igx_filter (AND); any=True: igx_filter_any (OR); any number of preds.
+    any=False: AND (MatchAll); any=True: OR (MatchAny); any number of preds.
+    nil_match=False: nil rows (valid == 0) are skipped (FilterEntries, filter.go:310-314);
+    True: a nil row evaluates Match(nil) == negate per pred (filter.go:286-291).
     Returns (idx u32 tensor of length n_selected)."""
     torch = torch_mod()
     ctx = context()
-    dev = cols[0].device if cols else "cuda"
+    dev = cols[0].device if cols else (valid.device if valid is not None else "cuda")
     ccols = (Col * max(1, len(cols)))(*[col_of(t, dtype_kind(t)) for t in cols])
     cpreds = (Pred * max(1, len(preds)))(*preds)
     out = torch.empty(max(1, n), dtype=torch.uint32, device=dev)
     cnt = torch.zeros(1, dtype=torch.uint64, device=dev)
-    fn = ctx.L.igx_filter_any if any else ctx.L.igx_filter
-    ctx.check(fn(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n, ptr(out), ptr(cnt)))
+    flags = (_abi.FILTER_ANY if any else 0) | (_abi.FILTER_NIL_MATCH if nil_match else 0)
+    ctx.check(ctx.L.igx_filter_ex(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n, flags,
+                                  ptr(out), ptr(cnt)))
     k = int(cnt.item())
     return out[:k]
 

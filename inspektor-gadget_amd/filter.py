@@ -3,10 +3,12 @@
 Same entry points and error texts as pkg/columns/filter/filter.go:
   GetFilterFromString (:91-172)    -> host parser in libigx.so (igx_filter_parse)
   GetFiltersFromStrings (:175-185) -> "invalid filter %q: %w"
-  FilterSpecs.MatchAll / MatchAny / FilterSpec.Match (:266-291) -> device scan
-  FilterEntries (:294-325)         -> sequential filters, nil rows skipped, order kept
-Regex rules (`~`) parse exactly as in the reference but the device scan rejects them
-with IGX_ENOTSUP (RE2 on the GPU is a SURVEY.md §8(f) "next" item).
+  FilterSpecs.MatchAll / MatchAny / FilterSpec.Match (:266-291) -> device scan, a nil row
+                                      giving Match(nil) == negate (:286-291)
+  FilterEntries (:294-325)         -> sequential filters, nil rows skipped, order kept; no
+                                      filters -> the never-assigned (nil) outEntries
+Regex rules (`~`) run on the device too: igx_filter compiles them on the host into a DFA
+over rune classes (igx_regex.cpp) that k_filter walks per row.
 """
 from __future__ import annotations
 
@@ -36,20 +38,25 @@ class FilterSpec:
         self.negate = bool(pred.negate)
 
     def Match(self, batch: EventBatch):
-        """Row ids of `batch` this filter matches (nil rows excluded)."""
-        return _scan(batch, [self])
+        """Row ids of `batch` this filter matches; a nil row matches iff the filter is
+        negated (filter.go:286-291)."""
+        return _scan(batch, [self], nil_match=True)
 
 
 class FilterSpecs(list):
     def MatchAll(self, batch: EventBatch):
-        return _scan(batch, list(self))
+        """filter.go:266-273 per row: a nil row is kept iff every spec is negated (or
+        there are none)."""
+        return _scan(batch, list(self), nil_match=True)
 
     def MatchAny(self, batch: EventBatch):
+        """filter.go:276-283 per row: no specs select nothing; a nil row is kept iff some
+        spec is negated."""
         torch = torch_mod()
         if not self:
             return torch.empty(0, dtype=torch.uint32, device=batch.device())
         return engine.filter_rows(batch.tensors_in_schema_order(), [s.pred for s in self],
-                                  batch.n, batch.valid, any=True)
+                                  batch.n, batch.valid, any=True, nil_match=True)
 
 
 def GetFilterFromString(cols: Columns, filt: str) -> FilterSpec:
@@ -74,26 +81,28 @@ def GetFiltersFromStrings(cols: Columns, filters) -> FilterSpecs:
     return out
 
 
-def _scan(batch: EventBatch, specs):
-    """AND of specs over the batch on the device (igx_filter: 4 predicates per mark launch,
-    later launches AND into the same bitmask); returns selected row ids (u32)."""
+def _scan(batch: EventBatch, specs, nil_match=False):
+    """AND of specs over the batch on the device (igx_filter_ex: 4 predicates per mark
+    launch, later launches AND into the same bitmask); returns selected row ids (u32).
+    nil_match=False skips nil rows (FilterEntries); True applies Match(nil) == negate."""
     return engine.filter_rows(batch.tensors_in_schema_order(), [s.pred for s in specs],
-                              batch.n, batch.valid)
+                              batch.n, batch.valid, nil_match=nil_match)
 
 
 def FilterEntries(cols: Columns, batch, filters):
-    """filter.go:294-325.  Returns the matching rows as a new batch (None for None)."""
+    """filter.go:294-325.  Returns the matching rows as a new batch, None for None (:295-297)
+    and None when there are no filters: the reference returns `outEntries`, which only the
+    filter loop assigns, so it is still the nil slice (:299,321-324)."""
     if batch is None:
         return None
-    out = batch
+    out = None
+    cur = batch
     for f in filters:
         try:
             fs = GetFilterFromString(cols, f)
         except FilterError as e:
             raise FilterError(f"could not apply filter {_go_q(f)}: {e}") from None
-        idx = _scan(out, [fs])
-        out = out.take(idx)
-    if not filters:
-        # no filters: the reference returns its (nil) outEntries slice
-        return batch.take(_scan(batch, [])) if batch.valid is not None else batch   # drops nil rows
+        idx = _scan(cur, [fs])
+        out = cur.take(idx)
+        cur = out
     return out

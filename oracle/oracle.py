@@ -256,6 +256,49 @@ def match_rows(preds, batch: dict, valid=None):
     return out[:k]
 
 
+def match_all(preds, batch: dict, valid=None):
+    """FilterSpecs.MatchAll applied to every entry (filter.go:266-273), nil entries included:
+    FilterSpec.Match(nil) returns its negate flag (:286-291), so a nil entry is kept iff every
+    spec is negated (vacuously with no specs).  Returns the kept row indices (np.uint32)."""
+    sel = match_rows(preds, batch, valid)
+    if valid is None or not all(p.negate for p in preds):
+        return sel
+    nil = np.nonzero(~np.asarray(valid).astype(bool))[0].astype(np.uint32)
+    return np.union1d(sel, nil).astype(np.uint32)
+
+
+def match_any(preds, batch: dict, valid=None):
+    """FilterSpecs.MatchAny per entry (filter.go:276-283): no specs keep nothing; a nil entry
+    is kept iff some spec is negated (Match(nil) == negate, :286-291)."""
+    if not preds:
+        return np.zeros(0, np.uint32)
+    sel = np.zeros(0, np.uint32)
+    for p in preds:
+        sel = np.union1d(sel, match_rows([p], batch, valid))
+    if valid is not None and any(p.negate for p in preds):
+        nil = np.nonzero(~np.asarray(valid).astype(bool))[0]
+        sel = np.union1d(sel, nil)
+    return sel.astype(np.uint32)
+
+
+def filter_entries(cols: dict, batch: dict, valid, filters):
+    """FilterEntries (filter.go:294-325) over SoA rows: returns the kept row ids in order, or
+    None where the reference returns a nil slice (nil input; no filters, since only the
+    filter loop assigns outEntries)."""
+    if batch is None:
+        return None
+    out = None
+    ids = np.arange(len(next(iter(batch.values()))), dtype=np.uint32)
+    v = None if valid is None else np.asarray(valid).astype(bool)
+    for f in filters:
+        p = parse_filter(cols, f)
+        sub = {k: np.asarray(a)[ids] for k, a in batch.items()}
+        keep = match_rows([p], sub, None if v is None else v[ids])
+        ids = ids[keep]
+        out = ids
+    return out
+
+
 # ------------------------------------------------------------------------------------
 # sort
 # ------------------------------------------------------------------------------------

@@ -41,3 +41,9 @@ def oracle():
     from oracle import oracle as O
     O.lib()
     return O
+
+
+@pytest.fixture(scope="session")
+def torch():
+    import torch as _torch
+    return _torch

@@ -74,6 +74,39 @@ def test_filter_multi_and_nil(oracle):
     assert p.negate is False
 
 
+def test_filter_entries_and_match_nil_semantics(oracle):
+    """FilterEntries (filter.go:294-325): nil input -> nil (filter_test.go:257-262), no
+    filters -> nil (outEntries is only assigned in the loop), table counts through the
+    reference's own route; MatchAll / MatchAny over a batch with a nil entry: the nil entry
+    is kept iff Match(nil) == negate holds for all / any specs (:266-291)."""
+    O = oracle
+    d, cols, batch, valid = _filter_fixture(O)
+    nil = int(np.nonzero(~valid)[0][0])
+    assert O.filter_entries(cols, None, None, [""]) is None
+    assert O.filter_entries(cols, batch, valid, []) is None
+    for row in d["rows"]:
+        if row["error"]:
+            continue
+        out = O.filter_entries(cols, batch, valid, [row["filter"]])
+        assert len(out) == row["count"] and nil not in out.tolist(), row
+        p = O.parse_filter(cols, row["filter"])
+        ma = O.match_all([p], batch, valid).tolist()
+        assert len(ma) == row["count"] + (1 if p.negate else 0), row
+        assert (nil in ma) == p.negate
+    # chained: the multi-filter case of filter_test.go:287-298
+    out = O.filter_entries(cols, batch, valid, d["multi"]["filters"])
+    assert len(out) == 1 and batch["int"][out[0]] == 1
+    neg = [O.parse_filter(cols, f) for f in ("int:!1", "int8:!2")]
+    pos = O.parse_filter(cols, "int:1")
+    assert nil in O.match_all(neg, batch, valid).tolist()
+    assert nil not in O.match_all(neg + [pos], batch, valid).tolist()
+    assert nil in O.match_all([], batch, valid).tolist()
+    assert len(O.match_all([], batch, valid)) == len(valid)
+    assert nil in O.match_any([pos, neg[0]], batch, valid).tolist()
+    assert nil not in O.match_any([pos], batch, valid).tolist()
+    assert len(O.match_any([], batch, valid)) == 0
+
+
 def test_filter_examples(oracle):
     """examples_test.go:24-89."""
     O = oracle
