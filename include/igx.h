@@ -342,6 +342,44 @@ int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
  * mod nparts (1..64).  part_counts (device u64[nparts]) receives the rows per part.  Async. */
 int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32_t row_bytes,
                        uint32_t key_bytes, uint32_t nparts, uint8_t *out, uint64_t *part_counts);
+/* ---- multi-GPU merges over RCCL ----------------------------------------
+ * One process per GPU.  Replaces the reference's node fan-out + client concatenation
+ * (pkg/runtime/grpc/grpc-runtime.go:221-237 -> pkg/snapshotcombiner/snapshotcombiner.go:79-106)
+ * with exact merges over xGMI.  Setup: rank 0 calls igx_dist_get_unique_id and hands the
+ * IGX_DIST_ID_BYTES bytes to every rank by the caller's own channel (ncclUniqueId); every rank
+ * then calls igx_dist_init on its context.  Collectives are enqueued on the context's stream
+ * and must be called in the same order on every rank.  The row exchanges all-gather their
+ * counts and capacities first (they synchronise the stream), so either every rank proceeds or
+ * every rank returns IGX_ENOSPC.  With out == NULL on every rank they are a size query: the
+ * counts are exchanged and returned, no rows move. */
+#define IGX_DIST_ID_BYTES 128
+typedef struct igx_dist igx_dist;
+int igx_dist_get_unique_id(uint8_t *out_id);
+int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int rank, igx_dist **out);
+int igx_dist_destroy(igx_dist *d);
+int igx_dist_rank(igx_dist *d, int *rank, int *nranks);
+int igx_dist_barrier(igx_dist *d);   /* synchronises */
+/* C3: in-place sum of a u32 buffer (log2 histograms) over all ranks (mod 2^32, exact).  Async. */
+int igx_dist_allreduce_u32(igx_dist *d, uint32_t *buf, uint64_t n);
+/* Top-K candidate merge (C2, C5): every rank's nrows x row_bytes rows (device) concatenated in
+ * rank order into out (device, cap_rows rows); counts (host, nranks, nullable) receives each
+ * rank's row count.  Feed the result to igx_topk with the rows' global first index as the
+ * position for the exact global top-K. */
+int igx_dist_allgather_rows(igx_dist *d, const void *rows, uint64_t nrows, uint32_t row_bytes, void *out,
+                            uint64_t cap_rows, uint64_t *counts);
+/* Group-by / distinct exchange (C4, C5): rows (device) already grouped by destination rank,
+ * send_counts[p] (host) rows for rank p in rank order, go to their rank; out (device,
+ * cap_rows rows) receives this rank's rows in source-rank order; recv_counts (host, nranks,
+ * nullable) their counts. */
+int igx_dist_alltoallv_rows(igx_dist *d, const void *rows, const uint64_t *send_counts, uint32_t row_bytes,
+                            void *out, uint64_t cap_rows, uint64_t *recv_counts);
+/* igx_partition_rows (owner = FNV-1a of the key words mod nranks) + igx_dist_alltoallv_rows:
+ * packed partial-group rows (igx_groupby_gather layout) go to the rank owning their key, which
+ * merges them with igx_groupby_update_ex (SUM of partials, MIN of first indices).  *out_nrows =
+ * rows received. */
+int igx_dist_exchange_groups(igx_dist *d, const void *rows, uint64_t nrows, uint32_t row_bytes,
+                             uint32_t key_bytes, void *out, uint64_t cap_rows, uint64_t *out_nrows);
+
 /* The step before the path: array-of-structs records on the device (a BPF
  * map dump of {key, value} structs or perf-ring event structs, e.g. tcptopIpKeyT +
  * tcptopTrafficT, pkg/gadgets/top/tcp/tracer/tcptop_bpfel_x86.go:15-30) are cut into SoA

@@ -74,6 +74,7 @@ class OpenCols(C.Structure):
 
 
 OPEN_SAMPLE_BYTES = 304
+DIST_ID_BYTES = 128
 
 
 class IgxError(RuntimeError):
@@ -127,6 +128,15 @@ SIGNATURES = [
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
     ("igx_partition_rows", _I, [_VP, _VP, _U64, _U32, _U32, _U32, _VP, _VP]),
+    ("igx_dist_get_unique_id", _I, [_VP]),
+    ("igx_dist_init", _I, [_VP, _VP, _I, _I, C.POINTER(_VP)]),
+    ("igx_dist_destroy", _I, [_VP]),
+    ("igx_dist_rank", _I, [_VP, C.POINTER(_I), C.POINTER(_I)]),
+    ("igx_dist_barrier", _I, [_VP]),
+    ("igx_dist_allreduce_u32", _I, [_VP, _VP, _U64]),
+    ("igx_dist_allgather_rows", _I, [_VP, _VP, _U64, _U32, _VP, _U64, C.POINTER(_U64)]),
+    ("igx_dist_alltoallv_rows", _I, [_VP, _VP, C.POINTER(_U64), _U32, _VP, _U64, C.POINTER(_U64)]),
+    ("igx_dist_exchange_groups", _I, [_VP, _VP, _U64, _U32, _U32, _VP, _U64, C.POINTER(_U64)]),
     ("igx_ingest_open_events", _I, [_VP, _VP, _U64, _U32, C.c_int64, C.POINTER(OpenCols)]),
     ("igx_ingest_aos", _I, [_VP, _VP, _U64, _U32, C.POINTER(_U32), C.POINTER(_U32), _U32,
                             C.POINTER(_VP)]),

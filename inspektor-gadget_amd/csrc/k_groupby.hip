@@ -1333,12 +1333,17 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     }
     t->koff = koff_of((int)t->kw_rec);
     t->krec_len = krec_bytes((int)t->kw_rec);
+    if (const char *d = std::getenv("IGX_GB_KR16"))   // tuning knob: 16-B rounded key records
+        if (std::strtoul(d, nullptr, 0)) t->krec_len = (uint32_t)igx_align(t->koff + 16, 16);
     t->vrec_len = vrec_bytes(naggs);
     t->naggs = naggs;
     for (uint32_t i = 0; i < naggs; ++i) t->aggs[i] = aggs[i];
     t->cap = capacity;
+    // S >= slotf/4 x capacity (default 2x); a smaller table stays resident in the Infinity Cache
+    uint64_t slotf = 8;
+    if (const char *d = std::getenv("IGX_GB_SLOTF")) slotf = std::max<uint64_t>(5, std::strtoul(d, nullptr, 0));
     uint64_t ns = 1024;
-    while (ns < 2 * capacity) ns <<= 1;
+    while (ns * 4 < slotf * capacity) ns <<= 1;
     t->nslots = ns;
     if (ns * t->krec_len >= (1ull << 32)) {
         const uint32_t r = t->krec_len;

@@ -1,8 +1,14 @@
 """Multi-GPU merges of the aggregation path.
 
-One process per GPU; `torch.distributed` carries the exchanges (backend "nccl" = RCCL over
-xGMI on MI355X; "gloo" in the CPU tests).  Only data movement and bookkeeping live here;
-every aggregation runs in libigx.so:
+One process per GPU.  Two transports carry the exchanges:
+
+  * RCCL through libigx.so's igx_dist_* C ABI (the same entry points a cgo caller binds):
+    used whenever the torch process group's backend is "nccl" (= RCCL over xGMI on MI355X).
+    torch.distributed only hands rank 0's ncclUniqueId to the other ranks.
+  * torch.distributed otherwise ("gloo": the CPU tests, and the ranks that share one GPU in
+    the world-size-2 GPU test); device tensors are staged through the host for gloo.
+
+Only data movement and bookkeeping live here; every aggregation and merge runs in libigx.so:
 
   log2 histograms (C3)      dense u32[keys][27] per rank -> all-reduce(sum)            exact
   group-by / distinct (C4)  local partial groups -> all-to-all by hash(key) -> the owner
@@ -17,7 +23,12 @@ an exact global merge is stricter and equal to the single-device result on the u
 """
 from __future__ import annotations
 
-from .runtime import torch_mod
+import ctypes as C
+import os
+
+from .runtime import torch_mod, context, ptr
+
+_comm = None
 
 
 def _dist():
@@ -31,35 +42,153 @@ def world():
     return (d.get_rank(), d.get_world_size()) if d else (0, 1)
 
 
-def allreduce_hist(hist):
-    """C3: in-place sum of a u32 histogram over ranks.  u32 addition mod 2^32 equals the
-    int32 two's-complement sum, so the buffer is reduced as int32 (RCCL and gloo)."""
+class TorchComm:
+    """torch.distributed transport (gloo, or any backend torch supports for these calls).
+    Device tensors go through the host when the backend is gloo."""
+
+    name = "torch"
+
+    def __init__(self, d):
+        self.d = d
+        self.stage = d.get_backend() == "gloo"
+
+    def _out(self, t):
+        return t.cpu() if self.stage and t.is_cuda else t
+
+    def allreduce_u32(self, hist):
+        torch = torch_mod()
+        h = self._out(hist)
+        self.d.all_reduce(h.view(torch.int32), op=self.d.ReduceOp.SUM)   # same bits mod 2^32
+        if h is not hist:
+            hist.copy_(h)
+        return hist
+
+    def allgather_rows(self, rows):
+        torch = torch_mod()
+        d, ws = self.d, self.d.get_world_size()
+        r = self._out(rows)
+        n = torch.tensor([r.shape[0]], dtype=torch.int64, device=r.device)
+        ns = [torch.empty_like(n) for _ in range(ws)]
+        d.all_gather(ns, n)
+        counts = [int(x.item()) for x in ns]
+        m = max(counts)
+        pad = torch.zeros((max(1, m), r.shape[1]), dtype=r.dtype, device=r.device)
+        if r.shape[0]:
+            pad[: r.shape[0]] = r
+        outs = [torch.empty_like(pad) for _ in range(ws)]
+        d.all_gather(outs, pad)
+        return torch.cat([o[:c] for o, c in zip(outs, counts)]).to(rows.device)
+
+    def alltoallv_rows(self, rows, counts):
+        torch = torch_mod()
+        d = self.d
+        r = self._out(rows)
+        send_counts = torch.tensor(counts, dtype=torch.int64, device=r.device)
+        recv_counts = torch.empty_like(send_counts)
+        d.all_to_all_single(recv_counts, send_counts)
+        rc = recv_counts.tolist()
+        out = torch.empty((sum(rc), r.shape[1]), dtype=r.dtype, device=r.device)
+        d.all_to_all_single(out, r.contiguous(), rc, list(counts))
+        return out.to(rows.device)
+
+
+class IgxComm:
+    """RCCL transport through libigx.so (igx_dist_*).  Rank 0's ncclUniqueId reaches the
+    other ranks over the torch process group; everything after that is the C ABI."""
+
+    name = "igx"
+
+    def __init__(self, d):
+        torch = torch_mod()
+        self.ctx = context()
+        L = self.ctx.L
+        from . import _abi
+        rank, ws = d.get_rank(), d.get_world_size()
+        uid = (C.c_uint8 * _abi.DIST_ID_BYTES)()
+        if rank == 0:
+            self.ctx.check(L.igx_dist_get_unique_id(uid))
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=torch.device("cuda", self.ctx.device))
+        d.broadcast(t, 0)
+        uid = (C.c_uint8 * _abi.DIST_ID_BYTES)(*t.cpu().tolist())
+        h = C.c_void_p()
+        self.ctx.check(L.igx_dist_init(self.ctx.h, uid, ws, rank, C.byref(h)))
+        self.h = h
+        self.ws = ws
+
+    def _bind(self):
+        self.ctx.bind_stream()
+        return self.ctx.L
+
+    def allreduce_u32(self, hist):
+        L = self._bind()
+        self.ctx.check(L.igx_dist_allreduce_u32(self.h, ptr(hist), hist.numel()))
+        return hist
+
+    def allgather_rows(self, rows):
+        torch = torch_mod()
+        L = self._bind()
+        rows = rows.contiguous()
+        n, rb = rows.shape
+        counts = (C.c_uint64 * self.ws)()
+        self.ctx.check(L.igx_dist_allgather_rows(self.h, ptr(rows), n, rb, None, 0, counts))   # size query
+        tot = sum(counts)
+        out = torch.empty((max(1, tot), rb), dtype=rows.dtype, device=rows.device)
+        self.ctx.check(L.igx_dist_allgather_rows(self.h, ptr(rows), n, rb, ptr(out), tot, counts))
+        return out[:tot]
+
+    def alltoallv_rows(self, rows, counts):
+        torch = torch_mod()
+        L = self._bind()
+        rows = rows.contiguous()
+        rb = rows.shape[1]
+        sc = (C.c_uint64 * self.ws)(*counts)
+        rc = (C.c_uint64 * self.ws)()
+        self.ctx.check(L.igx_dist_alltoallv_rows(self.h, ptr(rows), sc, rb, None, 0, rc))   # size query
+        tot = sum(rc)
+        out = torch.empty((max(1, tot), rb), dtype=rows.dtype, device=rows.device)
+        self.ctx.check(L.igx_dist_alltoallv_rows(self.h, ptr(rows), sc, rb, ptr(out), tot, rc))
+        return out[:tot]
+
+    def barrier(self):
+        self.ctx.check(self._bind().igx_dist_barrier(self.h))
+
+    def close(self):
+        if self.h:
+            self.ctx.L.igx_dist_destroy(self.h)
+            self.h = None
+
+
+def comm():
+    """The transport for the current process group (None without one).  IGX_DIST=torch
+    forces torch.distributed on an nccl group (diagnostics)."""
+    global _comm
     d = _dist()
     if d is None or d.get_world_size() == 1:
-        return hist
-    torch = torch_mod()
-    d.all_reduce(hist.view(torch.int32), op=d.ReduceOp.SUM)
-    return hist
+        return None
+    if _comm is None:
+        use_igx = d.get_backend() == "nccl" and os.environ.get("IGX_DIST", "igx") != "torch"
+        _comm = IgxComm(d) if use_igx else TorchComm(d)
+    return _comm
+
+
+def shutdown():
+    """Release the RCCL communicator (before destroy_process_group)."""
+    global _comm
+    if _comm is not None and hasattr(_comm, "close"):
+        _comm.close()
+    _comm = None
+
+
+def allreduce_hist(hist):
+    """C3: in-place sum of a u32 histogram over ranks."""
+    c = comm()
+    return hist if c is None else c.allreduce_u32(hist)
 
 
 def allgather_rows(rows):
     """Concatenate every rank's (n_r, row_bytes) uint8 rows in rank order (n_r may differ)."""
-    d = _dist()
-    if d is None or d.get_world_size() == 1:
-        return rows
-    torch = torch_mod()
-    ws = d.get_world_size()
-    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
-    ns = [torch.empty_like(n) for _ in range(ws)]
-    d.all_gather(ns, n)
-    counts = [int(x.item()) for x in ns]
-    m = max(counts)
-    pad = torch.zeros((max(1, m), rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    if rows.shape[0]:
-        pad[: rows.shape[0]] = rows
-    outs = [torch.empty_like(pad) for _ in range(ws)]
-    d.all_gather(outs, pad)
-    return torch.cat([o[:c] for o, c in zip(outs, counts)])
+    c = comm()
+    return rows if c is None else c.allgather_rows(rows)
 
 
 def partition_by_owner(rows, key_bytes, ws):
@@ -72,23 +201,13 @@ def partition_by_owner(rows, key_bytes, ws):
 def exchange_partitioned(rows, counts):
     """All-to-all of rows already grouped by destination rank (counts[r] rows for rank r,
     in rank order).  Returns the rows this rank owns, in source-rank order."""
-    d = _dist()
-    if d is None or d.get_world_size() == 1:
-        return rows
-    torch = torch_mod()
-    send_counts = torch.tensor(counts, dtype=torch.int64, device=rows.device)
-    recv_counts = torch.empty_like(send_counts)
-    d.all_to_all_single(recv_counts, send_counts)
-    rc = recv_counts.tolist()
-    out = torch.empty((sum(rc), rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    d.all_to_all_single(out, rows.contiguous(), rc, list(counts))
-    return out
+    c = comm()
+    return rows if c is None else c.alltoallv_rows(rows, counts)
 
 
 def exchange_rows(rows, key_bytes):
     """C4 group-by exchange: every partial-group row goes to the rank owning its key."""
-    d = _dist()
-    ws = 1 if d is None else d.get_world_size()
+    r, ws = world()
     if ws == 1:
         return rows
     part, counts = partition_by_owner(rows, key_bytes, ws)
@@ -111,21 +230,24 @@ def unpack_rows(rows, key_widths, naggs):
     return cols, aggs, first
 
 
-def merge_partials(rows, key_widths, out_widths, capacity):
+def merge_partials(rows, key_widths, out_widths, capacity, table=None):
     """Owner-side merge of exchanged partial groups on the device: one igx table whose
     aggregates SUM the partials and whose first index is the MIN of the partials' (the
     rows' u64 first column drives igx_groupby_update_ex's index column).  Returns the
-    engine.Table, finalized."""
+    engine.Table, finalized (`table`, when given, is reset and reused)."""
     from . import _abi, engine
     kcols, aggs, first = unpack_rows(rows, key_widths, len(out_widths))
     nk = len(kcols)
-    spec = [_abi.Agg(_abi.AGG_SUM, nk + x, _abi.NO_COL, ow, 0) for x, ow in enumerate(out_widths)]
-    tab = engine.Table(key_widths, spec, max(1, capacity))
+    if table is None:
+        spec = [_abi.Agg(_abi.AGG_SUM, nk + x, _abi.NO_COL, ow, 0) for x, ow in enumerate(out_widths)]
+        table = engine.Table(key_widths, spec, max(1, capacity))
+    else:
+        table.reset()
     n = rows.shape[0]
     if n:
-        tab.update(kcols + aggs + [first], list(range(nk)), n, 0, idx_col=nk + len(aggs))
-    tab.finalize()
-    return tab
+        table.update(kcols + aggs + [first], list(range(nk)), n, 0, idx_col=nk + len(aggs))
+    table.finalize()
+    return table
 
 
 def merge_topk(cand, key_bytes, naggs, sort_keys, k):

@@ -25,6 +25,28 @@ FILE_FIELDS = (("inode", "u64"), ("dev", "u32"), ("pid", "u32"), ("tid", "u32"),
                ("count", "u32"))
 
 
+def zipf_cdf(G: int, s: float):
+    """Host table for the generators: u63 fixed-point CDF thresholds of Zipf(s) over ranks
+    1..G (last == 1 << 63); k_gen.hip draws a rank by binary search of a u63 uniform."""
+    import numpy as np
+    k = np.arange(1, G + 1, dtype=np.float64)
+    c = np.cumsum(k ** (-s))
+    c /= c[-1]
+    out = np.minimum(np.floor(c * float(1 << 63)), float(1 << 63)).astype(np.uint64)
+    out[-1] = np.uint64(1 << 63)
+    return out
+
+
+def lognormal_quantiles(mu: float, sigma: float, nq: int = 4096, cap: int = 1 << 40):
+    """Host table for igx_gen_bio: nq+1 monotone quantile boundaries (u64 ns) of
+    lognormal(mu, sigma), capped (SURVEY.md §8(d) C3 latencies)."""
+    import numpy as np
+    from scipy.stats import norm
+    p = (np.arange(nq + 1, dtype=np.float64) + 0.5) / (nq + 1)
+    q = np.minimum(np.exp(mu + sigma * norm.ppf(p)), float(cap))
+    return np.maximum.accumulate(np.floor(q)).astype(np.uint64)
+
+
 def _alloc(fields, n, device):
     torch = torch_mod()
     dt = {"u8": torch.uint8, "u16": torch.uint16, "u32": torch.uint32, "u64": torch.uint64,

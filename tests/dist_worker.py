@@ -1,9 +1,10 @@
 """world_size-2 worker for tests/test_dist_cpu.py (gloo, CPU tensors).
 
-Runs the exchange code of inspektor-gadget_amd/dist.py for C3 (all-reduce), C4 (all-to-all
-by key owner + owner merge) and the top-K all-gather merge.  The per-rank aggregation that
-libigx.so does on a GPU is stood in for by the oracle here (no GPU in this container); the
-merges and the exchanged layouts are the product's.  Rank 0 checks every result against
+Runs the torch.distributed transport of inspektor-gadget_amd/dist.py (TorchComm) for C3
+(all-reduce), C4 (all-to-all by key owner) and the top-K all-gather.  There is no GPU in
+this container, so the per-rank aggregation and the owner-side merges that libigx.so does
+are stood in for by the oracle here; tests/test_gpu_dist.py runs the same exchanges with the
+product's aggregation, partition and merges on the GPU (two ranks sharing cuda:0).  Rank 0 checks every result against
 the oracle run over the union of all ranks' events and exits non-zero on a mismatch.
 """
 import importlib
@@ -71,8 +72,8 @@ def c4_exchange(rank, ws):
                                      base_idx=rank * N)
     rows = torch.from_numpy(rows_of(okeys, oaggs, ofirst))
     kb = okeys.shape[1]
-    # the device partition (igx_partition_rows) is checked against O.partition_rows in
-    # tests/test_gpu_dist_parts.py; here the oracle's grouping feeds the product's exchange
+    # the device partition (igx_partition_rows) runs in tests/dist_worker_gpu.py; here the
+    # oracle's grouping (same owner function) feeds the product's exchange
     part, counts = O.partition_rows(rows.numpy(), kb, ws)
     mine = D.exchange_partitioned(torch.from_numpy(part), counts)
     # every received key is owned by this rank

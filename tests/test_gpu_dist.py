@@ -1,0 +1,87 @@
+"""Multi-rank merges on the GPU.
+
+test_world2_product_merges: tests/dist_worker_gpu.py under torch.distributed.run, two ranks
+sharing cuda:0 over gloo (host-staged; RCCL refuses two ranks on one device): per-rank
+aggregation, partition, owner merge and top-K merge are libigx.so, checked against the oracle
+on the union of both ranks' events (C2, C3, C4, C5).
+
+test_igx_dist_rccl_single_rank: the igx_dist_* C ABI over RCCL with a one-rank communicator
+(the only RCCL shape a one-GPU box allows): unique id -> init -> all-reduce, all-gather, all-to-
+all (size queries and data), exchange_groups, capacity errors, barrier, destroy.
+"""
+import ctypes as C
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world2_product_merges():
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_worker_gpu.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "DIST_GPU_OK" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+
+
+def test_igx_dist_rccl_single_rank(igx, torch, oracle):
+    A, E, H = igx._abi, igx.engine, igx.columns
+    ctx = igx.runtime.context()
+    L = ctx.L
+    uid = (C.c_uint8 * A.DIST_ID_BYTES)()
+    assert L.igx_dist_get_unique_id(uid) == 0
+    h = C.c_void_p()
+    ctx.check(L.igx_dist_init(ctx.h, uid, 1, 0, C.byref(h)))
+    try:
+        r, n = C.c_int(-1), C.c_int(-1)
+        ctx.check(L.igx_dist_rank(h, C.byref(r), C.byref(n)))
+        assert (r.value, n.value) == (0, 1)
+        hist = torch.arange(4096 * 27, dtype=torch.int64, device="cuda").to(torch.int32).view(torch.uint32)
+        before = H.host(hist).copy()
+        ctx.check(L.igx_dist_allreduce_u32(h, C.c_void_p(hist.data_ptr()), hist.numel()))
+        torch.cuda.synchronize()
+        assert np.array_equal(H.host(hist), before)
+        rows = torch.randint(0, 256, (1000, 96), dtype=torch.uint8, device="cuda")
+        cnt = (C.c_uint64 * 1)()
+        ctx.check(L.igx_dist_allgather_rows(h, C.c_void_p(rows.data_ptr()), 1000, 96, None, 0, cnt))
+        assert cnt[0] == 1000
+        out = torch.empty_like(rows)
+        assert L.igx_dist_allgather_rows(h, C.c_void_p(rows.data_ptr()), 1000, 96, C.c_void_p(out.data_ptr()),
+                                         999, cnt) == A.IGX_ENOSPC
+        ctx.check(L.igx_dist_allgather_rows(h, C.c_void_p(rows.data_ptr()), 1000, 96, C.c_void_p(out.data_ptr()),
+                                            1000, cnt))
+        torch.cuda.synchronize()
+        assert torch.equal(out, rows)
+        sc = (C.c_uint64 * 1)(1000)
+        rc = (C.c_uint64 * 1)()
+        ctx.check(L.igx_dist_alltoallv_rows(h, C.c_void_p(rows.data_ptr()), sc, 96, None, 0, rc))
+        assert rc[0] == 1000
+        out2 = torch.empty_like(rows)
+        ctx.check(L.igx_dist_alltoallv_rows(h, C.c_void_p(rows.data_ptr()), sc, 96, C.c_void_p(out2.data_ptr()),
+                                            1000, rc))
+        torch.cuda.synchronize()
+        assert torch.equal(out2, rows)
+        got = C.c_uint64()
+        out3 = torch.empty_like(rows)
+        ctx.check(L.igx_dist_exchange_groups(h, C.c_void_p(rows.data_ptr()), 1000, 96, 72,
+                                             C.c_void_p(out3.data_ptr()), 1000, C.byref(got)))
+        torch.cuda.synchronize()
+        assert got.value == 1000 and torch.equal(out3, rows)   # one rank owns every key, order kept
+        ctx.check(L.igx_dist_barrier(h))
+    finally:
+        ctx.check(L.igx_dist_destroy(h))
