@@ -1,17 +1,26 @@
-"""Headline bench: top-tcp interval aggregation (BASELINE.json configs[1]).
+"""Headline bench: top-tcp interval aggregation (BASELINE.json configs[1]), plus the other
+SURVEY.md §8(d) configs in the same run.
 
-One step = one `top tcp` interval over a resident batch of synthetic events:
+One headline step = one `top tcp` interval over a resident batch of synthetic events:
   reset the device table (the per-interval map drain, tracer.go:154-171)
-  -> keyed group-by of every event on the 8-field ip_key_t, summing sent / recv
-     (tcptop.bpf.c:33-110; family filter :54-55 fused into the scan)
+  -> keyed group-by of every event on the 8-field ip_key_t, summing sent / recv, with the
+     probe's family set test fused in (tcptop.bpf.c:33-110; `family in {AF_INET, AF_INET6}`
+     :54-55 as an IGX_CMP_IN predicate, the same one gadgets.TopTcpTracer uses)
   -> stable top-20 by ["-sent","-recv"] with the reference's tie order (top.go:39-41)
   -> N>1: all-gather of the per-rank top-20 candidates over RCCL + exact global merge.
 Events are hash-partitioned across GPUs at ingest (each rank owns its own key universe),
 so per-GPU work is fixed as N grows ("scaling": "weak").
 
+The other configs (`--configs`, default c1,c3,c4,c5) run after the headline with their own
+timed steps and land in the line's "configs" object, each with its roofline and (rank 0,
+N=1) CPU baselines.  At N>1 their collectives are inside the timed region: C3 all-reduces
+the histogram, C4 and C5 exchange partial groups by key owner (every rank holds a slice of
+ONE global stream and key universe), C5 all-gathers the owners' top-20.
+
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the
 group-by kernel (HIP events on the stream it runs on) and `cpu_baseline` (the oracle's
-single-thread restatement of the reference's CPU path on a bounded sample, rank 0, N=1).
+restatement of the reference's CPU path on a bounded sample, all host cores, with the
+single-thread number beside it; rank 0, N=1).
 """
 import argparse
 import importlib
@@ -28,9 +37,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 METRIC = "events aggregated/sec (filter+group-by+top-K) at 1/2/4/8 MI355X; % HBM peak"   # BASELINE.json
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01", "traffic.json")   # tools/pmc_traffic.py
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 EV_BYTES = 71                  # saddr16 daddr16 mntns8 pid4 comm16 lport2 dport2 family2 size4 dir1
 GROUP_BYTES = 90               # key 66 + sent 8 + recv 8 + first_idx 8
+TCP_NAMES = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
 
 
 def parse():
@@ -43,9 +53,431 @@ def parse():
     p.add_argument("--zipf", type=float, default=1.1)
     p.add_argument("--topk", type=int, default=20)
     p.add_argument("--cpu-sample", type=int, default=48_000_000,
-                   help="events in the CPU-baseline sample (0 = skip); ~10 s single-thread")
+                   help="events in the C2 CPU-baseline sample (0 = skip every CPU baseline)")
+    p.add_argument("--configs", default="c1,c3,c4,c5",
+                   help="other configs to run after the headline ('' = none)")
+    p.add_argument("--config-events", type=int, default=125_000_000,
+                   help="events per GPU for C3/C4/C5 (the 8-GPU configs' 1B / 8)")
+    p.add_argument("--config-steps", type=int, default=5)
     p.add_argument("--check", action="store_true", help="verify the top-K against the oracle")
     return p.parse_args()
+
+
+class Timer:
+    """Wall time of K steps bracketed by barrier + synchronize, max over ranks; plus the
+    dominant kernel's HIP-event time on the stream it runs on."""
+
+    def __init__(self, torch, dist, world, dev):
+        self.torch, self.dist, self.world, self.dev = torch, dist, world, dev
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def run(self, step, steps, warmup):
+        for _ in range(warmup):
+            step(False)
+        self.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(True)
+        self.sync()
+        dt = time.perf_counter() - t0
+        if self.world > 1:
+            t = self.torch.tensor([dt], dtype=self.torch.float64, device=self.dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+
+class KernelClock:
+    """HIP events around the dominant kernel's launch on torch's current stream (the stream
+    libigx launches on: runtime.Context binds it); read after the timed loop, so timing adds
+    no host synchronisation to a step."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.pairs = []
+        self.on = False
+
+    def __enter__(self):
+        if self.on:
+            e0 = self.torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.pairs.append([e0, None])
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            e1 = self.torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.pairs[-1][1] = e1
+        return False
+
+    def avg(self):
+        if not self.pairs:
+            return float("nan")
+        self.torch.cuda.synchronize()
+        return float(np.mean([e0.elapsed_time(e1) for e0, e1 in self.pairs]))
+
+
+def roofline(alg_bytes, kernel_ms, kernel, alg_def, traffic_key, match):
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic, src = load_traffic(traffic_key, match)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel, "kernel_ms": kernel_ms,
+            "alg_bytes_per_launch": alg_bytes, "alg_bytes_def": alg_def, "traffic_source": src}
+
+
+def load_traffic(key, match):
+    """HBM bytes per launch of a config's dominant kernel, from the rocprofv3 PMC passes
+    committed under profiles/ (tools/pmc_traffic.py); None when absent or another config."""
+    path = os.path.join(PROFILE_DIR, f"traffic_{key}.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if any(t.get("config", {}).get(k) != v for k, v in match.items()):
+        return None, None
+    return t["traffic_bytes_per_launch"], os.path.relpath(path, ROOT) + " (bytes per launch)"
+
+
+def cpu_model():
+    try:
+        return [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
+    except Exception:
+        return platform.processor()
+
+
+def cpu_entry(units, single, multi, threads, unit, sample):
+    """cpu_baseline object: value = all host cores (the fair baseline), single_core beside it."""
+    return {"value": units / multi, "unit": unit, "cores": threads, "kind": "port", "sample": sample,
+            "single_core": {"value": units / single, "unit": unit, "cores": 1, "seconds": single},
+            "seconds": multi, "cpu": cpu_model(), "nproc": os.cpu_count()}
+
+
+# ------------------------------------------------------------------------------------
+# C2: the headline
+# ------------------------------------------------------------------------------------
+def family_in_pred(A, col):
+    """tcptop.bpf.c:54-55: drop unless family is AF_INET (2) or AF_INET6 (10)."""
+    p = A.Pred()
+    p.col, p.cmp, p.negate, p.ref_len = col, A.CMP_IN, 0, 4
+    for i, b in enumerate((2).to_bytes(2, "little") + (10).to_bytes(2, "little")):
+        p.ref[i] = b
+    return p
+
+
+def run_c2(a, ctx):
+    torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
+    rank, world = ctx["rank"], ctx["world"]
+    N, G, K = a.events, a.keys, a.topk
+    cdf_h = E.zipf_cdf(G, a.zipf)
+    base = rank * N                                   # global event index of row 0
+    ev = E.gen_tcp(0xC2, rank, G, H.to_device(cdf_h, ctx["dev"]), base, N)
+    cols = [ev[k] for k in TCP_NAMES]
+    aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
+    tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2], aggs, capacity=G + G // 4)
+    preds = [family_in_pred(A, 7)]
+    clk = KernelClock(torch)
+    st = {}
+
+    def step(record):
+        tab.reset()
+        clk.on = record
+        with clk:
+            tab.update(cols, list(range(8)), N, base, preds)
+        fin = tab.finalize()                          # syncs: group count for the top-K
+        # SortStats(["-sent","-recv"]) over the table's groups, first K slots
+        cand = tab.gather(tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K))
+        if world > 1:
+            cand = D.merge_topk(cand, 72, 2, [(0, True), (1, True)], K)
+        st["cand"], st["G"] = cand, fin["n_groups"]
+
+    torch.cuda.synchronize()
+    dt = T.run(step, a.steps, a.warmup)
+    Gn = st["G"]
+    alg = N * EV_BYTES + Gn * GROUP_BYTES
+    out = {"value": world * N * a.steps / dt, "ms_per_step": dt * 1000.0 / a.steps, "groups_per_gpu": Gn,
+           "roofline": roofline(alg, clk.avg(), "k_groupby<ip_key_t>",
+                                f"{EV_BYTES} B/event x events + {GROUP_BYTES} B/group x groups", "c2",
+                                {"events": N, "keys": G, "zipf": a.zipf})}
+    out["roofline"]["hbm_pct_of_peak_whole_step"] = 100.0 * alg / (out["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if a.check and rank == 0 and world == 1:
+        O = ctx["O"]
+        evh = O.gen_tcp(0xC2, 0, G, cdf_h, 0, N)
+        Gref, _, sent, recv, first = O.top_tcp(evh, K)
+        c = H.host(st["cand"])
+        ok = (np.array_equal(c[:, 88:96].copy().view(np.uint64).ravel(), first)
+              and np.array_equal(c[:, 72:80].copy().view(np.uint64).ravel(), sent)
+              and np.array_equal(c[:, 80:88].copy().view(np.uint64).ravel(), recv))
+        out["check"] = {"oracle_groups": int(Gref), "groups": int(Gn), "topk_bit_exact": bool(ok)}
+    if rank == 0 and world == 1 and a.cpu_sample:
+        O = ctx["O"]
+        S = a.cpu_sample
+        evh = O.gen_tcp(0xC2, 0, G, cdf_h, 0, S)
+        t0 = time.perf_counter()
+        r1 = O.top_tcp(evh, K)
+        single = time.perf_counter() - t0
+        thr = O.cpu_threads()
+        t0 = time.perf_counter()
+        r2 = O.top_tcp_mt(evh, K, threads=thr)
+        multi = time.perf_counter() - t0
+        assert np.array_equal(r1[4], r2[3]), "all-cores baseline disagrees with the single-thread one"
+        out["cpu_baseline"] = cpu_entry(
+            S, single, multi, thr, "events/s",
+            f"{S} events of the same stream (keys {G}, zipf {a.zipf}): oracle/igx_oracle.c or_top_tcp_mt "
+            f"(hash-partitioned Go-map restatement + per-thread SliceStable top-K + merge) on {thr} threads; "
+            f"single_core = or_top_tcp (BPF-map group-by, nextStats, SortEntries via Go SliceStable)")
+    tab.destroy()
+    return out
+
+
+# ------------------------------------------------------------------------------------
+# C1: pkg/columns FilterEntries + SortEntries over 1M trace-open events
+# ------------------------------------------------------------------------------------
+def run_c1(a, ctx):
+    torch, E, H, T = ctx["torch"], ctx["E"], ctx["H"], ctx["timer"]
+    igx = ctx["igx"]
+    n = 1_000_000
+    ev = E.gen_open(0xC1, H.to_device(E.zipf_cdf(64, 1.0), ctx["dev"]), ctx["rank"] * n, n)
+    cols = igx.columns.Columns([("pid", "uint32"), ("uid", "uint32"), ("mntns", "uint64"),
+                                ("comm", "string", 16), ("ret", "int64"), ("fd", "int64"),
+                                ("err", "int64"), ("path", "uint32")])
+    batch = igx.columns.EventBatch(cols, ev)
+    filters, sort_by = ["err:0", "pid:>=1000"], ["comm", "-pid"]
+    st = {}
+
+    def step(record):
+        out = igx.filter.FilterEntries(cols, batch, filters)
+        st["out"] = igx.sort.SortEntries(cols, out, sort_by)
+
+    dt = T.run(step, a.config_steps, 1)
+    sel = st["out"].n
+    ms = dt * 1000.0 / a.config_steps
+    alg = n * 12 + sel * 24
+    out = {"workload": "FilterEntries([err:0, pid:>=1000]) + SortEntries([comm, -pid]) of 1M trace-open events",
+           "events_per_gpu": n, "value": ctx["world"] * n / (ms * 1e-3), "unit": "events/s",
+           "ms_per_step": ms, "selected": sel,
+           "hbm_pct_of_peak_whole_step": 100.0 * alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "note": "launch- and sync-bound at 1M rows (several kernels, one host sync per filter)"}
+    if ctx["rank"] == 0 and ctx["world"] == 1 and a.cpu_sample:
+        O = ctx["O"]
+        h = O.gen_open(0xC1, O.zipf_cdf(64, 1.0), 0, n)
+        ocols = {"err": O.OCol("err", "int64", 8), "pid": O.OCol("pid", "uint32", 4)}
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            osel = O.match_rows([O.parse_filter(ocols, "err:0")], h)
+            osel = osel[O.match_rows([O.parse_filter(ocols, "pid:>=1000")], {"pid": h["pid"][osel]})]
+            O.go_sort_entries([(h["comm"][osel], "string", False), (h["pid"][osel], "uint32", True)], len(osel))
+        single = (time.perf_counter() - t0) / reps
+        out["cpu_baseline"] = {"value": n / single, "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": f"the full 1M-event batch x{reps}: oracle or_filter per filter + "
+                                         "or_sort_entries (Go SliceStable, one pass per key) -- the reference "
+                                         "path is single-threaded Go, so no all-cores variant",
+                               "cpu": cpu_model(), "nproc": os.cpu_count()}
+    return out
+
+
+# ------------------------------------------------------------------------------------
+# C3: profile block-io log2 histograms, all-reduce at N>1
+# ------------------------------------------------------------------------------------
+def run_c3(a, ctx):
+    torch, E, H, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["D"], ctx["timer"]
+    rank, world, n = ctx["rank"], ctx["world"], a.config_events
+    q = E.lognormal_quantiles(np.log(2e5), 1.5)
+    devs = [(8 << 20) | (16 * k) for k in range(16)]
+    ev = E.gen_bio(0xC3, H.to_device(q, ctx["dev"]), rank * n, n)
+    delta = ev["delta"].view(torch.int64)
+    hist = torch.zeros((4096, 27), dtype=torch.uint32, device=ctx["dev"])
+    clk = KernelClock(torch)
+
+    def step(record):
+        hist.zero_()
+        clk.on = record
+        with clk:
+            E.hist_log2(ev["dev"], ev["cont"], delta, devs, 256, hist=hist)
+        D.allreduce_hist(hist)
+
+    dt = T.run(step, a.config_steps, 1)
+    ms = dt * 1000.0 / a.config_steps
+    alg = n * 16 + 4096 * 27 * 4
+    out = {"workload": "profile block-io: log2 latency histograms, 16 devs x 256 containers x 27 slots"
+                       + (", RCCL all-reduce" if world > 1 else ""),
+           "events_per_gpu": n, "value": world * n / (ms * 1e-3), "unit": "events/s", "ms_per_step": ms,
+           "roofline": roofline(alg, clk.avg(), "k_hist", "16 B/event (dev 4, cont 4, delta 8) + 442 KB out",
+                                "c3", {"events": n}),
+           "total_counted": int(H.host(hist).astype(np.uint64).sum())}
+    if rank == 0 and world == 1 and a.cpu_sample:
+        O = ctx["O"]
+        S = 40_000_000
+        h = O.gen_bio(0xC3, q, 0, S)
+        t0 = time.perf_counter()
+        r1 = O.hist_log2(h["dev"], h["cont"], h["delta"], devs, 256)
+        single = time.perf_counter() - t0
+        thr = O.cpu_threads()
+        t0 = time.perf_counter()
+        r2 = O.hist_log2_mt(h["dev"], h["cont"], h["delta"], devs, 256, threads=thr)
+        multi = time.perf_counter() - t0
+        assert np.array_equal(r1, r2)
+        out["cpu_baseline"] = cpu_entry(S, single, multi, thr, "events/s",
+                                        f"{S} events of the same stream: or_hist_log2_mt (private histograms per "
+                                        f"thread, summed) on {thr} threads; single_core = or_hist_log2 "
+                                        "(biolatency.bpf.c:100-154 + bits.bpf.h log2l per event)")
+    return out
+
+
+# ------------------------------------------------------------------------------------
+# C4: advise network-policy distinct tuples, all-to-all by key owner at N>1
+# ------------------------------------------------------------------------------------
+def run_c4(a, ctx):
+    torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
+    rank, world, n = ctx["rank"], ctx["world"], a.config_events
+    names, widths = ("src", "pkt", "peer", "port"), [4, 1, 4, 2]
+    ev = E.gen_np(0xC4, 10_000, 100_000, rank * n, n, device=ctx["dev"])   # a slice of ONE global stream
+    cols = [ev[k] for k in names]
+    cap = 11_000_000
+    tab = E.Table(widths, [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], cap)
+    own = E.Table(widths, [A.Agg(A.AGG_SUM, 4, A.NO_COL, 8, 0)], cap) if world > 1 else None
+    clk = KernelClock(torch)
+    st = {}
+
+    def step(record):
+        tab.reset()
+        keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
+        clk.on = record
+        with clk:
+            tab.update(cols, [0, 1, 2, 3], n, rank * n, valid=keep)
+        fin = tab.finalize()
+        if world > 1:
+            rows = table_rows(E, torch, tab, fin)
+            mine = D.exchange_rows(rows, fin["key_bytes"])
+            D.merge_partials(mine, widths, [8], cap, table=own)
+            fin = own.fin
+        st["G"] = fin["n_groups"]
+
+    dt = T.run(step, a.config_steps, 1)
+    ms = dt * 1000.0 / a.config_steps
+    ng = st["G"]
+    alg = n * 24 + ng * 20
+    out = {"workload": "advise network-policy: np_mark + distinct (src, dir, peer, port) with first index"
+                       + (", partial groups all-to-all by key owner + owner merge" if world > 1 else ""),
+           "events_per_gpu": n, "value": world * n / (ms * 1e-3), "unit": "events/s", "ms_per_step": ms,
+           "distinct_on_rank0": ng,
+           "roofline": roofline(n * 24 + st["G"] * 20, clk.avg(), "k_groupby<np tuple>",
+                                "24 B/event (src 4, peer 4, port 2, pkt 1, type 1, proto 1, hostip 4, raddr 4, "
+                                "+3 pad) + 20 B/distinct tuple", "c4", {"events": n})}
+    out["roofline"]["alg_bytes_per_launch"] = alg
+    if rank == 0 and world == 1 and a.cpu_sample:
+        O = ctx["O"]
+        S = 20_000_000
+        h = O.gen_np(0xC4, 10_000, 100_000, 0, S)
+        keys = O.pad_keys(h, names)
+        keep = O.np_mark(h)
+        t0 = time.perf_counter()
+        k1, _, _ = O.groupby(keys, [{"kind": "count"}], valid=keep)
+        single = time.perf_counter() - t0
+        thr = O.cpu_threads()
+        t0 = time.perf_counter()
+        g2, _, _ = O.groupby_topk_mt(keys, [{"kind": "count"}], valid=keep, threads=thr)
+        multi = time.perf_counter() - t0
+        assert g2 == len(k1)
+        out["cpu_baseline"] = cpu_entry(S, single, multi, thr, "events/s",
+                                        f"{S} events of the same stream (keys pre-packed, not timed): "
+                                        f"or_groupby_topk_mt distinct on {thr} threads; single_core = or_groupby "
+                                        "(GeneratePolicies' first-event-wins map, advisor.go:279-320)")
+    tab.destroy()
+    if own is not None:
+        own.destroy()
+    return out
+
+
+def table_rows(E, torch, tab, fin):
+    """every occupied group of a finalized table as packed rows (key | aggs | first)."""
+    G = fin["n_groups"]
+    slots = torch.empty(max(1, G), dtype=torch.int32, device="cuda")[:G]
+    if G:
+        tab.ctx.check(tab.ctx.L.igx_memcpy_d2d(tab.ctx.h, slots.data_ptr(), fin["groups_ptr"], G * 4))
+    return tab.gather(slots)
+
+
+# ------------------------------------------------------------------------------------
+# C5: top file, 10M distinct keys, owner exchange + all-gather top-K at N>1
+# ------------------------------------------------------------------------------------
+def run_c5(a, ctx):
+    torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
+    rank, world, n = ctx["rank"], ctx["world"], a.config_events
+    G, K = 10_000_000, 20
+    names, widths = ("inode", "dev", "pid", "tid", "op", "count"), [8, 4, 4, 4]
+    cdf_h = E.zipf_cdf(G, 1.05)
+    ev = E.gen_file(0xC5, 0, G, H.to_device(cdf_h, ctx["dev"]), rank * n, n)   # one global key universe
+    cols = [ev[k] for k in names]
+    aggs = [A.Agg(A.AGG_COUNT, 0, 4, 8, 0), A.Agg(A.AGG_SUM, 5, 4, 8, 0),
+            A.Agg(A.AGG_COUNT, 0, 4, 8, 1), A.Agg(A.AGG_SUM, 5, 4, 8, 1)]
+    cap = G + G // 4
+    tab = E.Table(widths, aggs, cap)
+    own = E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], cap) if world > 1 else None
+    clk = KernelClock(torch)
+    st = {}
+
+    def step(record):
+        tab.reset()
+        clk.on = record
+        with clk:
+            tab.update(cols, [0, 1, 2, 3], n, rank * n)
+        fin = tab.finalize()
+        t = tab
+        if world > 1:
+            rows = table_rows(E, torch, tab, fin)
+            mine = D.exchange_rows(rows, fin["key_bytes"])
+            t = D.merge_partials(mine, widths, [8, 8, 8, 8], cap, table=own)
+        cand = t.gather(t.sort([(A.TSRC_AGG, 3, True)], K))       # ["-wbytes"]
+        if world > 1:
+            cand = D.merge_topk(cand, 20, 4, [(3, True)], K)
+        st["G"], st["cand"] = fin["n_groups"], cand
+
+    dt = T.run(step, a.config_steps, 1)
+    ms = dt * 1000.0 / a.config_steps
+    ng = st["G"]
+    alg = n * 25 + ng * 60
+    out = {"workload": "top file: group-by (inode, dev, pid, tid) with reads/rbytes/writes/wbytes, top-20 by "
+                       "[-wbytes]" + (", partial groups all-to-all by key owner, owners' top-20 all-gathered"
+                                      if world > 1 else ""),
+           "events_per_gpu": n, "keys": G, "value": world * n / (ms * 1e-3), "unit": "events/s",
+           "ms_per_step": ms, "groups_on_rank0": ng,
+           "roofline": roofline(alg, clk.avg(), "k_groupby<file_id>",
+                                "25 B/event (inode 8, dev 4, pid 4, tid 4, op 1, count 4) + 60 B/group", "c5",
+                                {"events": n, "keys": G})}
+    if rank == 0 and world == 1 and a.cpu_sample:
+        O = ctx["O"]
+        S = 10_000_000
+        h = O.gen_file(0xC5, 0, G, cdf_h, 0, S)
+        keys = O.pad_keys(h, ("inode", "dev", "pid", "tid"))
+        oaggs = [{"kind": "count", "cond": h["op"], "cond_val": 0},
+                 {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 0},
+                 {"kind": "count", "cond": h["op"], "cond_val": 1},
+                 {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 1}]
+        t0 = time.perf_counter()
+        _, oa, of = O.groupby(keys, oaggs)
+        perm = O.go_sort_entries([(oa[3], "uint64", True)], len(of))
+        single = time.perf_counter() - t0
+        thr = O.cpu_threads()
+        t0 = time.perf_counter()
+        _, first, _ = O.groupby_topk_mt(keys, oaggs, sort=[(3, True)], k=K, threads=thr)
+        multi = time.perf_counter() - t0
+        assert np.array_equal(first, of[perm[:K].astype(np.int64)])
+        out["cpu_baseline"] = cpu_entry(S, single, multi, thr, "events/s",
+                                        f"{S} events of the same stream (keys pre-packed, not timed): "
+                                        f"or_groupby_topk_mt on {thr} threads; single_core = or_groupby + "
+                                        "SortEntries([-wbytes]) via Go SliceStable over every group")
+    tab.destroy()
+    if own is not None:
+        own.destroy()
+    return out
 
 
 def main():
@@ -62,174 +494,50 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     igx = importlib.import_module("inspektor-gadget_amd")
-    from oracle import oracle as O   # only for the CDF table helper and the CPU baseline
-    E, H, A = igx.engine, igx.columns, igx._abi
+    O = None
+    if rank == 0 and world == 1 and (a.cpu_sample or a.check):
+        from oracle import oracle as O   # CPU baselines / --check only (test infrastructure)
+    ctx = {"torch": torch, "igx": igx, "E": igx.engine, "H": igx.columns, "A": igx._abi, "D": igx.dist,
+           "O": O, "rank": rank, "world": world, "dev": dev, "timer": Timer(torch, dist, world, dev)}
 
-    N, G, K = a.events, a.keys, a.topk
-    cdf_h = O.zipf_cdf(G, a.zipf)
-    cdf = H.to_device(cdf_h, dev)
-    base = rank * N                                   # global event index of row 0
-    ev = E.gen_tcp(0xC2, rank, G, cdf, base, N)
-    names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
-    cols = [ev[k] for k in names]
-    widths = [16, 16, 8, 4, 16, 2, 2, 2]
-    aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
-    tab = E.Table(widths, aggs, capacity=G + G // 4)
-    # BPF probe filter: family in {AF_INET, AF_INET6} (tcptop.bpf.c:54-55) -> family <= 10
-    fam = A.Pred()
-    fam.col, fam.cmp, fam.negate, fam.ref_len = 7, A.CMP_LE, 0, 2
-    fam.ref[0] = 10
-    preds = [fam]
-    torch.cuda.synchronize()
-
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    gb_ms = []
-
-    def step(record):
-        tab.reset()
-        if record:
-            ev0.record()
-        tab.update(cols, list(range(8)), N, base, preds)
-        if record:
-            ev1.record()
-        fin = tab.finalize()                          # syncs: group count for the top-K
-        Gn = fin["n_groups"]
-        # SortStats(["-sent","-recv"]) over the table's groups, first K slots
-        slots = tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K)
-        cand = tab.gather(slots)                      # K rows: key 72 | sent | recv | first
-        if world > 1:
-            out = [torch.empty_like(cand) for _ in range(world)]
-            dist.all_gather(out, cand)
-            allc = torch.cat(out)
-            cand = merge_candidates(E, H, allc, K)
-        if record:
-            gb_ms.append(ev0.elapsed_time(ev1))
-        return cand, Gn
-
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        cand, Gn = step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    ms_step = dt * 1000.0 / a.steps
-    value = world * N * a.steps / dt
-
-    gb_avg_ms = float(np.mean(gb_ms)) if gb_ms else float("nan")
-    alg_bytes = N * EV_BYTES + Gn * GROUP_BYTES
-    achieved = alg_bytes / (gb_avg_ms * 1e-3) / 1e9
-
-    traffic, traffic_src = load_traffic(N, G, a.zipf)
-
-    check = None
-    if a.check and rank == 0 and world == 1:
-        check = verify(O, cdf_h, G, N, K, cand, H)
+    c2 = run_c2(a, ctx)
+    configs = {}
+    for name in [c for c in a.configs.split(",") if c]:
+        fn = {"c1": run_c1, "c3": run_c3, "c4": run_c4, "c5": run_c5}[name]
+        configs[name] = fn(a, ctx)
+        torch.cuda.empty_cache()
 
     if rank == 0:
-        cpu = None
-        if a.cpu_sample and world == 1:
-            cpu = cpu_baseline(O, cdf_h, G, a.cpu_sample, K)
         line = {
             "metric": METRIC,
-            "value": value,
+            "value": c2["value"],
             "unit": "events/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": ms_step,
+            "ms_per_step": c2["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (counter-based SplitMix64 stream, Zipf key ranks)",
             "config": {
-                "workload": "top-tcp: filter family, group-by ip_key_t(saddr,daddr,mntns,pid,"
-                            "comm,lport,dport,family) sum sent/recv, stable top-20 by "
-                            "[-sent,-recv]",
-                "events_per_gpu": N, "keys_per_gpu": G, "zipf_s": a.zipf, "topk": K,
-                "groups_per_gpu": Gn,
+                "workload": "top-tcp: filter family in {AF_INET, AF_INET6}, group-by ip_key_t(saddr,daddr,mntns,"
+                            "pid,comm,lport,dport,family) sum sent/recv, stable top-20 by [-sent,-recv]",
+                "events_per_gpu": a.events, "keys_per_gpu": a.keys, "zipf_s": a.zipf, "topk": a.topk,
+                "groups_per_gpu": c2["groups_per_gpu"],
                 "parallelism": f"ingest-partitioned x{world}, RCCL all-gather top-K merge",
             },
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_groupby<ip_key_t>", "kernel_ms": gb_avg_ms,
-                "alg_bytes_per_launch": alg_bytes,
-                "alg_bytes_def": f"{EV_BYTES} B/event x events + {GROUP_BYTES} B/group x groups",
-                "traffic_source": traffic_src,
-                "hbm_pct_of_peak_whole_step": 100.0 * alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            },
-            "cpu_baseline": cpu,
+            "roofline": c2["roofline"],
+            "cpu_baseline": c2.get("cpu_baseline"),
+            "configs": configs,
         }
-        if check is not None:
-            line["check"] = check
+        if "check" in c2:
+            line["check"] = c2["check"]
         print(json.dumps(line), flush=True)
-    tab.destroy()
     if world > 1:
+        igx.dist.shutdown()
         dist.destroy_process_group()
-
-
-def load_traffic(N, G, zipf):
-    """HBM bytes per group-by launch measured by rocprofv3 PMC passes for this exact config
-    (tools/pmc_traffic.py output, committed under profiles/); None when absent."""
-    try:
-        with open(TRAFFIC_FILE) as fh:
-            t = json.load(fh)
-    except (OSError, ValueError):
-        return None, None
-    c = t.get("config", {})
-    if (c.get("events"), c.get("keys"), c.get("zipf")) != (N, G, zipf):
-        return None, None
-    return t["traffic_bytes_per_launch"], os.path.relpath(TRAFFIC_FILE, ROOT) + " (bytes per launch)"
-
-
-def merge_candidates(E, H, allc, K):
-    """Exact global top-K over all ranks' candidates (keys are rank-disjoint)."""
-    import torch
-    sent = allc[:, 72:80].contiguous().view(torch.uint64).flatten()
-    recv = allc[:, 80:88].contiguous().view(torch.uint64).flatten()
-    first = allc[:, 88:96].contiguous().view(torch.uint64).flatten()
-    idx = E.sort_perm([(sent, True), (recv, True)], allc.shape[0], pos=first, k=K)
-    return E.take([allc], idx)[0]
-
-
-def verify(O, cdf_h, G, N, K, cand, H):
-    ev = O.gen_tcp(0xC2, 0, G, cdf_h, 0, N)
-    Gref, keys, sent, recv, first = O.top_tcp(ev, K)
-    c = H.host(cand)
-    got_first = c[:, 88:96].copy().view(np.uint64).flatten()
-    got_sent = c[:, 72:80].copy().view(np.uint64).flatten()
-    ok = bool(np.array_equal(got_first, first) and np.array_equal(got_sent, sent))
-    return {"oracle_groups": int(Gref), "topk_bit_exact": ok}
-
-
-def cpu_baseline(O, cdf_h, G, S, K):
-    """Single-thread restatement of the reference CPU path (BPF-map group-by per event,
-    nextStats drain, SortEntries(-sent,-recv) via Go SliceStable, truncate) on S events."""
-    ev = O.gen_tcp(0xC2, 0, G, cdf_h, 0, S)
-    t0 = time.perf_counter()
-    O.top_tcp(ev, K)
-    dt = time.perf_counter() - t0
-    try:
-        cpu_model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":")[1].strip()
-    except Exception:
-        cpu_model = platform.processor()
-    return {"value": S / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"{S} events of the same stream (keys {G}, zipf), oracle/igx_oracle.c "
-                      f"or_top_tcp single thread, {dt:.2f} s",
-            "cpu": cpu_model, "nproc": os.cpu_count()}
 
 
 if __name__ == "__main__":

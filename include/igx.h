@@ -195,7 +195,10 @@ int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, const char *con
 /* Sort permutation with the exact tie order of Go 1.19 sort.SliceStable under
  * getLessFunc (SURVEY.md §0.3 closed form).  pos (device u64, nullable): pre-sort position
  * of each row (NULL = row index).  valid (device, nullable): nil rows sort last.
- * out_perm (device u32, nrows).  Asynchronous. */
+ * Float keys compare as Go's `<` does: -0 == +0, -Inf < finite < +Inf; a NaN in a float key
+ * of a non-nil row makes the comparison unordered (no strict weak order, so SliceStable's
+ * output depends on its merge steps) and the call returns IGX_ENOTSUP.
+ * out_perm (device u32, nrows).  Synchronises once (key range scan); otherwise async. */
 int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                   const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm);
 

@@ -37,6 +37,7 @@ struct ComposeArgs {
     const uint8_t *valid;
     const uint32_t *rowmap;
     uint64_t n, stride;   // stride = words array pitch (elements)
+    uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN
 };
 
 __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, uint32_t j) {
@@ -71,11 +72,13 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
             if (a.width[k] == 4) {
                 uint32_t b = *reinterpret_cast<const uint32_t *>(p);
+                if ((b & 0x7FFFFFFFu) > 0x7F800000u) *a.nan_seen = 1u;   // unordered: see launch_sort_perm
                 if (b == 0x80000000u) b = 0;                       // -0 == +0 in Go
                 b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
                 words[w * a.stride + i] = b ^ inv;
             } else {
                 uint64_t b = *reinterpret_cast<const uint64_t *>(p);
+                if ((b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull) *a.nan_seen = 1u;
                 if (b == 0x8000000000000000ull) b = 0;
                 b = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
                 words[w * a.stride + i] = (uint32_t)(b >> 32) ^ inv;
@@ -644,7 +647,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
                           igx_align(((size_t)256 * nblocks + SCAN_CHUNK - 1) / SCAN_CHUNK * 4, 256);
     constexpr uint32_t ANDOR_BLOCKS = 256;
-    const size_t res_b = igx_align((size_t)KW * 8, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
+    const size_t res_b = igx_align((size_t)KW * 8 + 4, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     void *s;
@@ -659,16 +662,24 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     uint32_t *res = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b);
 
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
+    ca.nan_seen = res + 2 * KW;
+    IGX_HIP(ctx, hipMemsetAsync(ca.nan_seen, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
     const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
-    uint32_t *apart = res + igx_align((size_t)KW * 2, 64);
+    uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
     hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart);
     hipLaunchKernelGGL(k_andor_final, dim3(KW), dim3(TB), 0, ctx->stream, apart, ablocks, res);
     uint32_t *hres;
-    rc = igx_pinned(ctx, KW * 8, reinterpret_cast<void **>(&hres));
+    rc = igx_pinned(ctx, KW * 8 + 4, reinterpret_cast<void **>(&hres));
     if (rc) return rc;
-    IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8 + 4, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    // Go's `<` is unordered on NaN, so getLessFunc (sort.go:125-135) is no strict weak order
+    // once a NaN is present and SliceStable's result depends on its insertion-sort blocks and
+    // symMerge steps, not on the values alone: no radix order reproduces it.
+    if (hres[2 * KW])
+        return igx_fail(ctx, IGX_ENOTSUP, "sort: NaN in a float sort key (Go's SliceStable order under an "
+                                          "unordered comparison is not reproduced)");
 
     if (use_sel) {
         // top-K: radix select on the composed keys, then rank the k survivors

@@ -583,3 +583,359 @@ u64 or_top_tcp(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 *pi
     free(perm); free(keys); free(sent); free(recv); free(first);
     return G;
 }
+
+/* ------------------------------------------------------------------------------------
+ * 7. All-cores CPU baselines (bench.py cpu_baseline, SURVEY.md §8(d) "all host cores with
+ *    the C++ restatement, which is fair").  Same results as the single-thread paths above:
+ *      phase 1  each thread scans a contiguous slice of the events, builds each key and
+ *               appends the event index to bucket[thread][owner], owner = hash(key) mod T
+ *      phase 2  thread j aggregates every event of owner j in global index order (so the
+ *               first index it sees for a key is the key's first occurrence)
+ *      phase 3  thread j sorts its groups (first-occurrence order) with the Go SliceStable
+ *               restatement and keeps the first k
+ *      merge    the T x k candidates, in first-occurrence order, sorted once more: equal
+ *               to sorting every group, since the sort order is a total order on
+ *               (keys, position) under the closed form
+ * ---------------------------------------------------------------------------------- */
+#include <pthread.h>
+
+typedef struct {
+    u64 *first;           /* per group */
+    u64 *agg;             /* naggs x cap, group-major rows of naggs */
+    u8 *keys;
+    u64 cap;
+} mt_groups;
+
+typedef struct mt_job mt_job;
+struct mt_job {
+    /* key source: packed keys (kb bytes per row) or the top-tcp columns (ip_key_t) */
+    const u8 *keys;
+    u32 kb;
+    const u8 *saddr, *daddr, *comm;
+    const u64 *mntns;
+    const u32 *pid;
+    const u16 *lport, *dport, *family;
+    const u8 *valid;
+    const or_agg *aggs;
+    u32 naggs;
+    u64 n, base_idx;
+    u32 T;
+    const u32 *sort_agg, *sort_desc;
+    u32 nsort, k;
+    pthread_barrier_t bar;
+    u32 **bucket;         /* T x T arrays of event indices */
+    u64 *bcnt, *bcap;     /* T x T */
+    u64 *G;               /* groups per owner */
+    u64 *cand_first;      /* T x k */
+    u64 *cand_agg;        /* T x k x naggs */
+    u64 *cand_n;          /* per owner */
+    u64 *csum;            /* per owner: sum of group_csum over its groups (top tcp only) */
+    int want_csum;
+    int oom;
+};
+
+static inline u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+/* Order-independent fingerprint of one top-tcp group: FNV-1a-64 over the key fields in
+ * ip_key_t order without padding (saddr 16, daddr 16, mntns 8, pid 4, comm 16, lport 2,
+ * dport 2, family 2 = 66 bytes), xor sent/recv/first times odd constants, splitmix64
+ * finalised.  The full-table checksum is the u64 sum over groups (tests/test_gpu_fullsize.py
+ * computes the same from the device table). */
+static u64 group_csum(const ip_key_t *k, u64 sent, u64 recv, u64 first) {
+    u8 b[66];
+    memcpy(b, k->saddr, 16); memcpy(b + 16, k->daddr, 16); memcpy(b + 32, &k->mntns, 8);
+    memcpy(b + 40, &k->pid, 4); memcpy(b + 44, k->name, 16); memcpy(b + 60, &k->lport, 2);
+    memcpy(b + 62, &k->dport, 2); memcpy(b + 64, &k->family, 2);
+    u64 h = 14695981039346656037ull;
+    for (int i = 0; i < 66; i++) { h ^= b[i]; h *= 1099511628211ull; }
+    return mix64(h ^ (sent * 0x9E3779B97F4A7C15ull) ^ (recv * 0xC2B2AE3D27D4EB4Full) ^ (first * 0x165667B19E3779F9ull));
+}
+
+typedef struct { mt_job *job; u32 t; } mt_arg;
+
+static inline void mt_key(const mt_job *J, u64 i, u8 *buf) {
+    if (J->keys) { memcpy(buf, J->keys + (u64)J->kb * i, J->kb); return; }
+    ip_key_t *k = (ip_key_t *)buf;
+    memset(k, 0, sizeof *k);
+    memcpy(k->saddr, J->saddr + 16 * i, 16);
+    memcpy(k->daddr, J->daddr + 16 * i, 16);
+    k->mntns = J->mntns[i]; k->pid = J->pid[i];
+    memcpy(k->name, J->comm + 16 * i, 16);
+    k->lport = J->lport[i]; k->dport = J->dport[i]; k->family = J->family[i];
+}
+
+static inline int mt_keep(const mt_job *J, u64 i) {
+    if (J->valid && !J->valid[i]) return 0;
+    if (J->family && J->family[i] != 2 && J->family[i] != 10) return 0;   /* tcptop.bpf.c:54-55 */
+    return 1;
+}
+
+static int mt_push(mt_job *J, u64 b, u32 v) {
+    if (J->bcnt[b] == J->bcap[b]) {
+        u64 nc = J->bcap[b] ? 2 * J->bcap[b] : 4096;
+        u32 *p = (u32 *)realloc(J->bucket[b], nc * 4);
+        if (!p) return -1;
+        J->bucket[b] = p;
+        J->bcap[b] = nc;
+    }
+    J->bucket[b][J->bcnt[b]++] = v;
+    return 0;
+}
+
+/* growing map: slot -> group id + 1, rehash from the stored hash */
+static int mt_grow(or_map *m) {
+    u64 cap = m->cap * 2;
+    u32 *slot = (u32 *)calloc(cap, 4);
+    u64 *hash = (u64 *)malloc(cap * 8);
+    if (!slot || !hash) { free(slot); free(hash); return -1; }
+    for (u64 s = 0; s < m->cap; s++) {
+        if (!m->slot[s]) continue;
+        u64 d = m->hash[s] & (cap - 1);
+        while (slot[d]) d = (d + 1) & (cap - 1);
+        slot[d] = m->slot[s];
+        hash[d] = m->hash[s];
+    }
+    free(m->slot); free(m->hash);
+    m->slot = slot; m->hash = hash; m->cap = cap; m->mask = cap - 1;
+    return 0;
+}
+
+static int mt_groups_fit(mt_groups *g, u64 need, u32 kb, u32 naggs) {
+    if (need <= g->cap) return 0;
+    u64 nc = g->cap ? 2 * g->cap : 1 << 16;
+    while (nc < need) nc *= 2;
+    u8 *k = (u8 *)realloc(g->keys, nc * kb);
+    if (k) g->keys = k;
+    u64 *f = (u64 *)realloc(g->first, nc * 8);
+    if (f) g->first = f;
+    u64 *a = (u64 *)realloc(g->agg, nc * 8 * (naggs ? naggs : 1));
+    if (a) g->agg = a;
+    if (!k || !f || !a) return -1;
+    g->cap = nc;
+    return 0;
+}
+
+static void *mt_worker(void *p) {
+    mt_arg *A = (mt_arg *)p;
+    mt_job *J = A->job;
+    const u32 T = J->T, t = A->t, kb = J->keys ? J->kb : (u32)sizeof(ip_key_t), na = J->naggs;
+    u8 buf[256];
+    /* phase 1: partition this thread's slice by owner */
+    const u64 lo = J->n * t / T, hi = J->n * (t + 1) / T;
+    for (u64 i = lo; i < hi; i++) {
+        if (!mt_keep(J, i)) continue;
+        mt_key(J, i, buf);
+        const u64 h = fnv(buf, kb);
+        if (mt_push(J, (u64)t * T + (u32)((h >> 32) % T), (u32)i)) { J->oom = 1; break; }
+    }
+    pthread_barrier_wait(&J->bar);
+    /* phase 2: aggregate owner t's events in global index order */
+    or_map m;
+    mt_groups g = {0};
+    if (J->oom || map_init(&m, 1 << 15, kb)) { J->oom = 1; pthread_barrier_wait(&J->bar); return NULL; }
+    for (u32 s = 0; s < T && !J->oom; s++) {
+        const u64 b = (u64)s * T + t;
+        for (u64 e = 0; e < J->bcnt[b]; e++) {
+            const u64 i = J->bucket[b][e];
+            mt_key(J, i, buf);
+            if (m.n * 2 >= m.cap && mt_grow(&m)) { J->oom = 1; break; }
+            if (mt_groups_fit(&g, m.n + 1, kb, na)) { J->oom = 1; break; }
+            int is_new;
+            const u64 gi = map_find_or_insert(&m, buf, g.keys, &is_new);
+            if (is_new) {
+                g.first[gi] = J->base_idx + i;
+                for (u32 a = 0; a < na; a++) g.agg[gi * na + a] = 0;
+            }
+            for (u32 a = 0; a < na; a++) {
+                const or_agg *G = &J->aggs[a];
+                if (G->cond_width && ld_u(G->cond, G->cond_width, i) != G->cond_val) continue;
+                u64 add = G->kind == OR_AGG_COUNT ? 1 : ld_u(G->val, G->val_width, i);
+                if (G->kind != OR_AGG_COUNT && G->val_signed && G->val_width < 8) {
+                    const u32 sh = 64 - 8 * G->val_width;
+                    add = (u64)(((int64_t)(add << sh)) >> sh);
+                }
+                if (G->kind != OR_AGG_COUNT && G->div > 1) add /= G->div;
+                u64 v = g.agg[gi * na + a] + add;
+                if (G->out_width < 8) v &= (1ull << (8 * G->out_width)) - 1;
+                g.agg[gi * na + a] = v;
+            }
+        }
+    }
+    const u64 Gt = m.n;
+    map_free(&m);
+    J->G[t] = Gt;
+    if (J->want_csum && !J->oom && na == 2) {
+        u64 cs = 0;
+        for (u64 x = 0; x < Gt; x++)
+            cs += group_csum((const ip_key_t *)(g.keys + (u64)kb * x), g.agg[x * 2], g.agg[x * 2 + 1], g.first[x]);
+        J->csum[t] = cs;
+    }
+    /* phase 3: SortStats over this owner's groups (first-occurrence order), keep k */
+    if (!J->oom && J->k && Gt) {
+        u32 *perm = (u32 *)malloc(Gt * 4);
+        u64 *col = (u64 *)malloc(Gt * 8 * (J->nsort ? J->nsort : 1));
+        or_sortkey ks[8];
+        if (!perm || !col) { J->oom = 1; }
+        else {
+            for (u64 x = 0; x < Gt; x++) perm[x] = (u32)x;
+            for (u32 s = 0; s < J->nsort && s < 8; s++) {
+                for (u64 x = 0; x < Gt; x++) col[s * Gt + x] = g.agg[x * na + J->sort_agg[s]];
+                ks[s].ptr = col + s * Gt; ks[s].width = 8; ks[s].kind = OR_UINT; ks[s].desc = J->sort_desc[s];
+            }
+            or_sort_entries(perm, Gt, NULL, ks, J->nsort);
+            const u64 m2 = Gt < J->k ? Gt : J->k;
+            for (u64 r = 0; r < m2; r++) {
+                J->cand_first[(u64)t * J->k + r] = g.first[perm[r]];
+                for (u32 a = 0; a < na; a++) J->cand_agg[((u64)t * J->k + r) * na + a] = g.agg[(u64)perm[r] * na + a];
+            }
+            J->cand_n[t] = m2;
+        }
+        free(perm); free(col);
+    }
+    free(g.keys); free(g.first); free(g.agg);
+    pthread_barrier_wait(&J->bar);
+    return NULL;
+}
+
+static int cmp_u64_pair(const void *a, const void *b) {
+    const u64 x = ((const u64 *)a)[0], y = ((const u64 *)b)[0];
+    return x < y ? -1 : x > y;
+}
+
+/* Returns the number of groups ((u64)-1 on allocation failure); out_first / out_agg
+ * (k x naggs) receive the first k rows of the sorted groups. */
+static u64 mt_run_csum(mt_job *J, u64 *out_first, u64 *out_agg, u64 *out_csum);
+static u64 mt_run(mt_job *J, u64 *out_first, u64 *out_agg) { return mt_run_csum(J, out_first, out_agg, NULL); }
+static u64 mt_run_csum(mt_job *J, u64 *out_first, u64 *out_agg, u64 *out_csum) {
+    const u32 T = J->T ? J->T : 1, na = J->naggs;
+    J->T = T;
+    J->oom = 0;
+    J->bucket = (u32 **)calloc((u64)T * T, sizeof(u32 *));
+    J->bcnt = (u64 *)calloc((u64)T * T, 8);
+    J->bcap = (u64 *)calloc((u64)T * T, 8);
+    J->G = (u64 *)calloc(T, 8);
+    J->cand_first = (u64 *)calloc((u64)T * (J->k ? J->k : 1), 8);
+    J->cand_agg = (u64 *)calloc((u64)T * (J->k ? J->k : 1) * (na ? na : 1), 8);
+    J->cand_n = (u64 *)calloc(T, 8);
+    J->csum = (u64 *)calloc(T, 8);
+    pthread_t *th = (pthread_t *)malloc(T * sizeof(pthread_t));
+    mt_arg *args = (mt_arg *)malloc(T * sizeof(mt_arg));
+    u64 G = (u64)-1;
+    if (J->bucket && J->bcnt && J->bcap && J->G && J->cand_first && J->cand_agg && J->cand_n && th && args) {
+        pthread_barrier_init(&J->bar, NULL, T);
+        for (u32 t = 0; t < T; t++) { args[t].job = J; args[t].t = t; }
+        for (u32 t = 1; t < T; t++) pthread_create(&th[t], NULL, mt_worker, &args[t]);
+        mt_worker(&args[0]);
+        for (u32 t = 1; t < T; t++) pthread_join(th[t], NULL);
+        pthread_barrier_destroy(&J->bar);
+        if (!J->oom) {
+            G = 0;
+            for (u32 t = 0; t < T; t++) G += J->G[t];
+            /* merge: candidates in first-occurrence order, then the same sort */
+            u64 nc = 0;
+            for (u32 t = 0; t < T; t++) nc += J->cand_n[t];
+            if (J->k && nc) {
+                u64 *rec = (u64 *)malloc(nc * 8 * (1 + na));
+                u64 w = 0;
+                for (u32 t = 0; t < T; t++)
+                    for (u64 r = 0; r < J->cand_n[t]; r++, w++) {
+                        rec[w * (1 + na)] = J->cand_first[(u64)t * J->k + r];
+                        for (u32 a = 0; a < na; a++) rec[w * (1 + na) + 1 + a] = J->cand_agg[((u64)t * J->k + r) * na + a];
+                    }
+                qsort(rec, nc, 8 * (1 + na), cmp_u64_pair);
+                u32 *perm = (u32 *)malloc(nc * 4);
+                u64 *col = (u64 *)malloc(nc * 8 * (J->nsort ? J->nsort : 1));
+                or_sortkey ks[8];
+                for (u64 x = 0; x < nc; x++) perm[x] = (u32)x;
+                for (u32 s = 0; s < J->nsort && s < 8; s++) {
+                    for (u64 x = 0; x < nc; x++) col[s * nc + x] = rec[x * (1 + na) + 1 + J->sort_agg[s]];
+                    ks[s].ptr = col + s * nc; ks[s].width = 8; ks[s].kind = OR_UINT; ks[s].desc = J->sort_desc[s];
+                }
+                or_sort_entries(perm, nc, NULL, ks, J->nsort);
+                for (u64 r = 0; r < J->k && r < nc; r++) {
+                    out_first[r] = rec[(u64)perm[r] * (1 + na)];
+                    for (u32 a = 0; a < na; a++) out_agg[r * na + a] = rec[(u64)perm[r] * (1 + na) + 1 + a];
+                }
+                free(perm); free(col); free(rec);
+            }
+        }
+    }
+    if (out_csum && J->csum && G != (u64)-1) {
+        *out_csum = 0;
+        for (u32 t = 0; t < T; t++) *out_csum += J->csum[t];
+    }
+    free(J->csum);
+    if (J->bucket)
+        for (u64 b = 0; b < (u64)T * T; b++) free(J->bucket[b]);
+    free(J->bucket); free(J->bcnt); free(J->bcap); free(J->G); free(J->cand_first); free(J->cand_agg);
+    free(J->cand_n); free(th); free(args);
+    return G;
+}
+
+/* top tcp on T threads: out_* as or_top_tcp (keys omitted), same rows. */
+u64 or_top_tcp_mt(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 *pid,
+                  const u8 *comm, const u16 *lport, const u16 *dport, const u16 *family,
+                  const u32 *size, const u8 *dir, u64 n, u64 base_idx, u32 nthreads, u32 k,
+                  u64 *out_sent, u64 *out_recv, u64 *out_first, u64 *out_csum) {
+    or_agg aggs[2] = {{OR_AGG_SUM, 4, size, 1, dir, 0, 8, 0, 0}, {OR_AGG_SUM, 4, size, 1, dir, 1, 8, 0, 0}};
+    const u32 sa[2] = {0, 1}, sd[2] = {1, 1};   /* ["-sent", "-recv"] */
+    mt_job J;
+    memset(&J, 0, sizeof J);
+    J.saddr = saddr; J.daddr = daddr; J.mntns = mntns; J.pid = pid; J.comm = comm;
+    J.lport = lport; J.dport = dport; J.family = family;
+    J.aggs = aggs; J.naggs = 2; J.n = n; J.base_idx = base_idx; J.T = nthreads;
+    J.sort_agg = sa; J.sort_desc = sd; J.nsort = 2; J.k = k;
+    J.want_csum = out_csum != NULL;
+    u64 *agg = (u64 *)malloc((k ? k : 1) * 16);
+    const u64 G = mt_run_csum(&J, out_first, agg, out_csum);
+    for (u32 r = 0; r < k && G != (u64)-1 && r < G; r++) { out_sent[r] = agg[2 * r]; out_recv[r] = agg[2 * r + 1]; }
+    free(agg);
+    return G;
+}
+
+/* generic keyed aggregation + top-k by aggregates (sort_agg[s], sort_desc[s] in sortBy
+ * order; nsort 0 / k 0 = group count only) on T threads. */
+u64 or_groupby_topk_mt(const u8 *keys, u32 kb, u64 n, const u8 *valid, const or_agg *aggs, u32 naggs,
+                       u64 base_idx, u32 nthreads, const u32 *sort_agg, const u32 *sort_desc, u32 nsort,
+                       u32 k, u64 *out_first, u64 *out_agg) {
+    mt_job J;
+    memset(&J, 0, sizeof J);
+    J.keys = keys; J.kb = kb; J.valid = valid; J.aggs = aggs; J.naggs = naggs; J.n = n;
+    J.base_idx = base_idx; J.T = nthreads; J.sort_agg = sort_agg; J.sort_desc = sort_desc;
+    J.nsort = nsort; J.k = k;
+    return mt_run(&J, out_first, out_agg);
+}
+
+/* log2 histograms on T threads: private histograms per slice, summed (u32 wrap). */
+typedef struct {
+    const u32 *dev, *cont; const i64 *delta; u64 lo, hi; const u32 *devs; u32 ndev, ncont; u64 divisor;
+    u32 nslots; u32 *hist;
+} hist_arg;
+static void *hist_worker(void *p) {
+    hist_arg *h = (hist_arg *)p;
+    or_hist_log2(h->dev ? h->dev + h->lo : NULL, h->cont ? h->cont + h->lo : NULL, h->delta + h->lo,
+                 h->hi - h->lo, h->devs, h->ndev, h->ncont, h->divisor, h->nslots, h->hist);
+    return NULL;
+}
+void or_hist_log2_mt(const u32 *dev, const u32 *cont, const i64 *delta, u64 n, const u32 *devs,
+                     u32 ndev, u32 ncont, u64 divisor, u32 nslots, u32 *hist, u32 nthreads) {
+    const u32 T = nthreads ? nthreads : 1;
+    const u64 keys = (u64)(ndev ? ndev : 1) * ncont * nslots;
+    u32 *priv = (u32 *)calloc((u64)T * keys, 4);
+    pthread_t *th = (pthread_t *)malloc(T * sizeof(pthread_t));
+    hist_arg *a = (hist_arg *)malloc(T * sizeof(hist_arg));
+    for (u32 t = 0; t < T; t++) {
+        a[t] = (hist_arg){dev, cont, delta, n * t / T, n * (t + 1) / T, devs, ndev, ncont, divisor, nslots,
+                          priv + (u64)t * keys};
+        if (t) pthread_create(&th[t], NULL, hist_worker, &a[t]);
+    }
+    hist_worker(&a[0]);
+    for (u32 t = 1; t < T; t++) pthread_join(th[t], NULL);
+    for (u32 t = 0; t < T; t++)
+        for (u64 x = 0; x < keys; x++) hist[x] += priv[(u64)t * keys + x];
+    free(priv); free(th); free(a);
+}

@@ -74,6 +74,13 @@ def _declare(L):
                                C.c_uint32, vp]
     L.or_top_tcp.argtypes = [vp] * 10 + [u64, u64, u64, C.c_uint32, vp, vp, vp, vp]
     L.or_top_tcp.restype = u64
+    L.or_top_tcp_mt.argtypes = [vp] * 10 + [u64, u64, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    L.or_top_tcp_mt.restype = u64
+    L.or_groupby_topk_mt.argtypes = [vp, C.c_uint32, u64, vp, vp, C.c_uint32, u64, C.c_uint32, vp, vp,
+                                     C.c_uint32, C.c_uint32, vp, vp]
+    L.or_groupby_topk_mt.restype = u64
+    L.or_hist_log2_mt.argtypes = [vp, vp, vp, u64, vp, C.c_uint32, C.c_uint32, u64, C.c_uint32, vp,
+                                  C.c_uint32]
 
 
 # ------------------------------------------------------------------------------------
@@ -978,3 +985,98 @@ def partition_rows(rows, key_bytes, ws):
     owner = key_owner(np.ascontiguousarray(rows[:, :key_bytes]), ws)
     order = np.argsort(owner, kind="stable")
     return np.ascontiguousarray(rows[order]), np.bincount(owner, minlength=ws).tolist()
+
+
+# ------------------------------------------------------------------------------------
+# all-cores CPU baselines (igx_oracle.c §7): same results as the single-thread paths
+# ------------------------------------------------------------------------------------
+def cpu_threads():
+    """Host threads a baseline may use: the process's CPU affinity, capped by
+    OMP_NUM_THREADS when set (the GPU box's per-GPU CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def top_tcp_mt(ev, k=20, base_idx=0, threads=None, checksum=False):
+    """or_top_tcp on `threads` threads (hash-partitioned by key).  Returns (G, sent, recv,
+    first) of the first k sorted rows, plus the full-table checksum (tcp_group_checksum
+    summed over every group) when `checksum`."""
+    T = threads or cpu_threads()
+    n = len(ev["pid"])
+    sent, recv, first = (np.empty(k, np.uint64) for _ in range(3))
+    cs = np.zeros(1, np.uint64)
+    cols = [np.ascontiguousarray(ev[c]) for c in ("saddr", "daddr", "mntns", "pid", "comm",
+                                                  "lport", "dport", "family", "size", "dir")]
+    G = lib().or_top_tcp_mt(*[_p(c) for c in cols], n, base_idx, T, k, _p(sent), _p(recv), _p(first),
+                            _p(cs) if checksum else None)
+    m = min(k, G)
+    out = (G, sent[:m], recv[:m], first[:m])
+    return out + (int(cs[0]),) if checksum else out
+
+
+def tcp_group_checksum(fields66, sent, recv, first):
+    """numpy twin of igx_oracle.c group_csum summed over groups: fields66 (G, 66) uint8 are
+    the key fields in ip_key_t order without padding."""
+    with np.errstate(over="ignore"):
+        h = np.full(len(sent), 14695981039346656037, np.uint64)
+        for i in range(66):
+            h ^= fields66[:, i].astype(np.uint64)
+            h *= np.uint64(1099511628211)
+        z = h ^ (sent * np.uint64(0x9E3779B97F4A7C15)) ^ (recv * np.uint64(0xC2B2AE3D27D4EB4F)) ^ \
+            (first * np.uint64(0x165667B19E3779F9))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        z = z ^ (z >> np.uint64(31))
+        return int(z.sum(dtype=np.uint64))
+
+
+def groupby_topk_mt(keys_packed, aggs, valid=None, base_idx=0, sort=(), k=0, threads=None):
+    """or_groupby_topk_mt: keyed aggregation (aggs as for groupby) + the first k groups
+    sorted by [(agg index, desc)] on `threads` threads.  Returns (G, first (k,), aggs (k, naggs))."""
+    T = threads or cpu_threads()
+    keys_packed = np.ascontiguousarray(keys_packed, dtype=np.uint8)
+    n, kb = keys_packed.shape
+    cag, hold = [], []
+    for a in aggs:
+        val, cond = a.get("val"), a.get("cond")
+        if val is not None:
+            val = np.ascontiguousarray(val)
+            hold.append(val)
+        if cond is not None:
+            cond = np.ascontiguousarray(cond)
+            hold.append(cond)
+        cag.append(_CAgg(0 if a["kind"] == "count" else 1, 0 if val is None else val.dtype.itemsize,
+                         0 if val is None else val.ctypes.data, 0 if cond is None else cond.dtype.itemsize,
+                         0 if cond is None else cond.ctypes.data, int(a.get("cond_val", 0)),
+                         int(a.get("out_width", 8)), int(val is not None and val.dtype.kind == "i"),
+                         int(a.get("div", 0))))
+    arr = (_CAgg * max(1, len(cag)))(*cag)
+    sa = np.array([x for x, _ in sort] or [0], np.uint32)
+    sd = np.array([int(d) for _, d in sort] or [0], np.uint32)
+    first = np.zeros(max(1, k), np.uint64)
+    out = np.zeros((max(1, k), max(1, len(aggs))), np.uint64)
+    v8 = None if valid is None else np.ascontiguousarray(valid.astype(np.uint8))
+    G = lib().or_groupby_topk_mt(_p(keys_packed), kb, n, _p(v8), C.cast(arr, C.c_void_p), len(cag), base_idx,
+                                 T, _p(sa), _p(sd), len(sort), k, _p(first), _p(out))
+    if G == (1 << 64) - 1:
+        raise MemoryError("or_groupby_topk_mt")
+    m = min(k, G)
+    return G, first[:m], out[:m, :len(aggs)]
+
+
+def hist_log2_mt(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, threads=None):
+    T = threads or cpu_threads()
+    devs = np.ascontiguousarray(devs, dtype=np.uint32)
+    hist = np.zeros((max(1, len(devs)) * ncont, nslots), dtype=np.uint32)
+    delta = np.ascontiguousarray(delta).view(np.int64)
+    dev = np.ascontiguousarray(np.zeros(len(delta), np.uint32) if dev is None else dev, dtype=np.uint32)
+    cont = np.ascontiguousarray(np.zeros(len(delta), np.uint32) if cont is None else cont, dtype=np.uint32)
+    lib().or_hist_log2_mt(_p(dev), _p(cont), _p(delta), len(dev), _p(devs), len(devs), ncont, divisor, nslots,
+                          _p(hist), T)
+    return hist

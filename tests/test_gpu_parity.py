@@ -1,8 +1,8 @@
 """GPU parity: libigx.so (through the C ABI) vs the CPU oracle on identical seeded streams.
 
 Bit-exact for everything (integer counting, keying and ordering).  Sizes are chosen so
-the oracle finishes in seconds; full-size runs are covered by the property tests in
-tests/test_gpu_properties.py.
+the oracle finishes in seconds; the headline config at full size (100M events) is
+tests/test_gpu_fullsize.py.
 """
 import numpy as np
 import pytest
@@ -250,3 +250,42 @@ def test_hist_log2_c3(oracle, E, H, torch):
                               divisor=1_000_000))
     ref2 = oracle.hist_log2(ev_h["dev"], ev_h["cont"], ev_h["delta"], devs[3:9], 100, divisor=1_000_000)
     assert np.array_equal(got2, ref2)
+
+
+def test_float_sort_keys_match_go(oracle, igx, torch):
+    """Float sort keys (sort.go:71-74 getLessFunc[float32/float64]): Go's `<` -- -0 == +0
+    (a tie), -Inf < finite < +Inf, subnormals ordered -- under ASC / DESC and mixed with an int
+    key, against the Go 1.19 SliceStable restatement; heavy ties exercise the closed form's
+    tie parity.  A NaN makes the comparison unordered: IGX_ENOTSUP."""
+    E, H, A = igx.engine, igx.columns, igx._abi
+    rng = np.random.default_rng(11)
+    n = 50_000
+    pool32 = np.array([0.0, -0.0, np.inf, -np.inf, 1.5, -1.5, 1e-45, -1e-45, 3.4e38, -3.4e38, 7.0, 7.0],
+                      np.float32)
+    pool64 = np.array([0.0, -0.0, np.inf, -np.inf, 2.5, -2.5, 5e-324, -5e-324, 1.7e308, 1.0 / 3.0],
+                      np.float64)
+    f32 = pool32[rng.integers(0, len(pool32), n)]
+    f64 = np.where(rng.random(n) < 0.5, pool64[rng.integers(0, len(pool64), n)], rng.standard_normal(n))
+    i8 = rng.integers(-3, 3, n).astype(np.int8)
+    d32, d64, di8 = H.to_device(f32), H.to_device(f64), H.to_device(i8)
+    cases = [[(0, False)], [(0, True)], [(1, False)], [(1, True)], [(0, True), (2, False)],
+             [(2, True), (0, False), (1, True)], [(0, False), (1, False)]]
+    cols = [(d32, f32, "float32"), (d64, f64, "float64"), (di8, i8, "int8")]
+    for keys in cases:
+        got = H.host(E.sort_perm([(cols[c][0], desc) for c, desc in keys], n)).astype(np.int64)
+        ref = oracle.go_sort_entries([(cols[c][1], cols[c][2], desc) for c, desc in keys], n).astype(np.int64)
+        assert np.array_equal(got, ref), keys
+        k = 25
+        top = H.host(E.sort_perm([(cols[c][0], desc) for c, desc in keys], n, k=k)).astype(np.int64)
+        assert np.array_equal(top, ref[:k]), keys
+    bad = f64.copy()
+    bad[123] = np.nan
+    with pytest.raises(A.IgxError) as ei:
+        E.sort_perm([(H.to_device(bad), False)], n)
+    assert ei.value.code == A.IGX_ENOTSUP
+    # a NaN in a nil row is never compared (sort.go:127-132 returns before reading the field)
+    valid = np.ones(n, np.uint8)
+    valid[123] = 0
+    got = H.host(E.sort_perm([(H.to_device(bad), True)], n, valid=H.to_device(valid))).astype(np.int64)
+    ref = oracle.go_sort_entries([(bad, "float64", True)], n, valid=valid).astype(np.int64)
+    assert np.array_equal(got, ref)
