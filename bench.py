@@ -341,8 +341,10 @@ def run_c4(a, ctx):
     ev = E.gen_np(0xC4, 10_000, 100_000, rank * n, n, device=ctx["dev"])   # a slice of ONE global stream
     cols = [ev[k] for k in names]
     cap = 11_000_000
-    tab = E.Table(widths, [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], cap)
-    own = E.Table(widths, [A.Agg(A.AGG_SUM, 4, A.NO_COL, 8, 0)], cap) if world > 1 else None
+    # distinct only, as the reference: graph.c:102-114 (BPF_NOEXIST, first timestamp wins),
+    # advisor.go:307-319 (first event per tuple); nothing is counted
+    tab = E.Table(widths, [], cap)
+    own = E.Table(widths, [], cap) if world > 1 else None
     clk = KernelClock(torch)
     st = {}
 
@@ -356,7 +358,7 @@ def run_c4(a, ctx):
         if world > 1:
             rows = table_rows(E, torch, tab, fin)
             mine = D.exchange_rows(rows, fin["key_bytes"])
-            D.merge_partials(mine, widths, [8], cap, table=own)
+            D.merge_partials(mine, widths, [], cap, table=own)
             fin = own.fin
         st["G"] = fin["n_groups"]
 
@@ -370,7 +372,7 @@ def run_c4(a, ctx):
            "distinct_on_rank0": ng,
            "roofline": roofline(n * 24 + st["G"] * 20, clk.avg(), "k_groupby<np tuple>",
                                 "24 B/event (src 4, peer 4, port 2, pkt 1, type 1, proto 1, hostip 4, raddr 4, "
-                                "+3 pad) + 20 B/distinct tuple", "c4", {"events": n})}
+                                "+3 pad) + 20 B/distinct tuple (key 12 + first 8)", "c4", {"events": n})}
     out["roofline"]["alg_bytes_per_launch"] = alg
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
@@ -379,11 +381,11 @@ def run_c4(a, ctx):
         keys = O.pad_keys(h, names)
         keep = O.np_mark(h)
         t0 = time.perf_counter()
-        k1, _, _ = O.groupby(keys, [{"kind": "count"}], valid=keep)
+        k1, _, _ = O.groupby(keys, [], valid=keep)
         single = time.perf_counter() - t0
         thr = O.cpu_threads()
         t0 = time.perf_counter()
-        g2, _, _ = O.groupby_topk_mt(keys, [{"kind": "count"}], valid=keep, threads=thr)
+        g2, _, _ = O.groupby_topk_mt(keys, [], valid=keep, threads=thr)
         multi = time.perf_counter() - t0
         assert g2 == len(k1)
         out["cpu_baseline"] = cpu_entry(S, single, multi, thr, "events/s",

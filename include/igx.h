@@ -289,6 +289,16 @@ int igx_groupby_finalize(igx_table *t, igx_table_view *view);
  * igx_groupby_finalize.  Asynchronous. */
 int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows);
 int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete loop) */
+/* How updates run (results are identical in every mode):
+ *   IGX_GB_CACHED  one workgroup per CU with an LDS cache of hot keys (Zipf-like streams:
+ *                  most rows never leave the CU);
+ *   IGX_GB_DIRECT  every row probes the HBM table itself (near-uniform, high-cardinality
+ *                  streams, where nearly every row would miss the cache);
+ *   IGX_GB_AUTO    (default) cached; an interval in which more than 90% of the rows missed
+ *                  the cache switches the next 16 intervals to direct, then measures again.
+ * The mode of an interval is fixed by its first update. */
+enum igx_gb_mode { IGX_GB_AUTO = 0, IGX_GB_CACHED = 1, IGX_GB_DIRECT = 2 };
+int igx_groupby_set_mode(igx_table *t, uint32_t mode);
 /* SortStats over the table's groups (same order as igx_sort_perm with pos = first_idx);
  * writes the first k (0 = all) group slots to out_slots (device u32).  Call after
  * igx_groupby_finalize.  Asynchronous. */

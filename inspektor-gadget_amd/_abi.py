@@ -24,6 +24,7 @@ NO_COL = 0xFFFFFFFF
 MAX_REF = 256
 AGG_COUNT, AGG_SUM = 0, 1
 FILTER_ANY, FILTER_NIL_MATCH = 1, 2
+GB_AUTO, GB_CACHED, GB_DIRECT = 0, 1, 2
 
 
 class SchemaCol(C.Structure):
@@ -122,6 +123,7 @@ SIGNATURES = [
     ("igx_segment_fsum", _I, [_VP, _VP, _U32, _U32, _VP, _U64, _VP, _VP, _U32, _VP]),
     ("igx_ip_text", _I, [_VP, _VP, _U32, _VP, _U32, _VP, _U64, _VP]),
     ("igx_groupby_reset", _I, [_VP]),
+    ("igx_groupby_set_mode", _I, [_VP, _U32]),
     ("igx_groupby_destroy", _I, [_VP]),
     ("igx_groupby_debug_counts", _I, [_VP, _VP]),
     ("igx_np_mark", _I, [_VP, _VP, _VP, _VP, _VP, _U64, _VP]),

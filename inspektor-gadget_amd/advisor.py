@@ -116,7 +116,9 @@ class NetworkPolicyAdvisor:
         enc = self.encode()
         ev = {k: H.to_device(v) for k, v in enc.items()}
         keep = engine.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
-        tab = engine.Table([4, 1, 4, 2], [_abi.Agg(_abi.AGG_COUNT, 0, _abi.NO_COL, 8, 0)], n)
+        # distinct only: graph.c:102-114 inserts with BPF_NOEXIST and the advisor keeps the first
+        # event per tuple (advisor.go:307-319); nothing is counted
+        tab = engine.Table([4, 1, 4, 2], [], n)
         try:
             tab.update([ev["src"], ev["pkt"], ev["peer"], ev["port"]], [0, 1, 2, 3], n, 0, valid=keep)
             fin = tab.finalize()

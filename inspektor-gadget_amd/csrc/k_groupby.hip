@@ -45,6 +45,9 @@
 
 namespace {
 
+#ifndef IGX_GB_DIRECT_U
+#define IGX_GB_DIRECT_U 2
+#endif
 constexpr uint32_t SLOT_OVF = 0xFFFFFFFFu;
 constexpr int KWMAX = 32;
 constexpr int AMAX = 4;   // top file needs 4 (reads, rbytes, writes, wbytes)
@@ -296,7 +299,7 @@ __device__ __forceinline__ void probe_issue(const GbArgs &a, uint64_t h, uint32_
 }
 
 // d holds the home slot's record (probe_issue)
-template <int KW>
+template <int KW, bool SET_OCC = true>
 __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
                                                    uint64_t gidx, uint64_t &first_ins,
                                                    uint32_t (&d)[probe_quads<KW>() * 4]) {
@@ -315,12 +318,18 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
             const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF),
                                            (unsigned long long)t, (unsigned long long)tag);
             if (old == t) {
+                // key words as 16-byte write-through stores (each store is one memory-side write)
 #pragma unroll
-                for (int w = 0; w < KW; w += 2) {
-                    if (w + 1 < KW)
+                for (int w = 0; w < KW; w += 4) {
+                    if (w + 3 < KW) {
+                        const u4v q = {k[w], k[w + 1], k[w + 2], k[w + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + 4 * w, 0, 16 /* sc1 */);
+                    } else if (w + 1 < KW) {
                         st_agent(reinterpret_cast<uint64_t *>(r + 4 * w), (uint64_t)k[w] | ((uint64_t)k[w + 1] << 32));
-                    else
+                        if (w + 2 < KW) st_agent(reinterpret_cast<uint32_t *>(r + 4 * w + 8), k[w + 2]);
+                    } else {
                         st_agent(reinterpret_cast<uint32_t *>(r + 4 * w), k[w]);
+                    }
                 }
                 // the value record starts at first = first_ins, aggregates 0 (no reset pass)
                 uint64_t *vr = a.vrec + s * a.vrec_words;
@@ -328,7 +337,7 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                 for (uint32_t x = 1; x < a.vrec_words; ++x) st_agent(vr + x, 0ull);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), (a.ep << 48) | (gidx + 1));
-                atomicOr(a.occ + (s >> 5), 1u << (s & 31));
+                if (SET_OCC) atomicOr(a.occ + (s >> 5), 1u << (s & 31));
                 first_ins = gidx;
                 return (uint32_t)s;
             }
@@ -1132,6 +1141,54 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     }
 }
 
+// ---- direct form: no LDS cache ---------------------------------------------------------
+// For near-uniform, high-cardinality streams (C4's distinct tuples: nearly every row misses
+// any per-CU cache) the LDS cache, its rings and its roles only add work: every row goes
+// to HBM anyway.  Here each lane takes rows of a grid-stride sweep (so the whole grid
+// advances through the stream in index order and first indices arrive nearly in order --
+// the atomicMin on `first` is then rare) and resolves each one itself: probe, compare,
+// claim, atomics.  The throughput is the chip's random-access rate (~45-50 G probes/s over
+// a 1 GiB table, tools/micro/randacc.hip); occupancy, not a pipeline, hides the latency.
+template <class L, int NA>
+__global__ __launch_bounds__(256) void k_groupby_direct(GbArgs a) {
+    constexpr int KW = L::KW;
+    constexpr int U = IGX_GB_DIRECT_U;   // rows in flight per lane: all rows' loads, then all probes
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t row0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; row0 < a.n; row0 += U * stride) {
+        RowRaw<L, NA> R[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t row = row0 + u * stride;
+            issue_row<L, NA>(a, row < a.n ? row : row0, R[u]);
+        }
+        uint32_t k[U][KW];
+        uint64_t v[U][NA], h[U];
+        bool ok[U];
+        uint32_t d[U][probe_quads<KW>() * 4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t row = row0 + u * stride;
+            ok[u] = row < a.n && decode_row<L, NA>(a, row, R[u], k[u], v[u]);
+            h[u] = hash_key<KW>(k[u]);
+            if (ok[u]) probe_issue<KW>(a, h[u], d[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint64_t gidx = row_gidx(a, row0 + u * stride);
+            uint64_t first_ins = 0;
+            // no occupancy bit: finalize rebuilds the bitmap from the tags (k_occ_from_tags),
+            // one streaming pass instead of a memory-side atomic per claim
+            const uint32_t gs = find_or_insert<KW, false>(a, k[u], h[u], gidx, first_ins, d[u]);
+            if (gs == SLOT_OVF) continue;
+#pragma unroll
+            for (int x = 0; x < NA; ++x)
+                if (x < (int)a.naggs && v[u][x]) gadd(rec_agg(a, gs, x), (unsigned long long)v[u][x]);
+            if (gidx < first_ins) gmin(rec_first(a, gs), (unsigned long long)gidx);
+        }
+    }
+}
+
 // Full clear of tags and `ready` (keys and value records are left as is).  Needed only
 // when the epoch counter wraps: every other interval starts by bumping the epoch.
 __global__ void k_table_clear(uint8_t *krec, uint32_t krec_len, uint32_t koff, uint64_t ns) {
@@ -1142,6 +1199,24 @@ __global__ void k_table_clear(uint8_t *krec, uint32_t krec_len, uint32_t koff, u
 
 // ---- finalize: list the occupied slots in ascending order, from the occupancy bitmap ----
 constexpr int CT = 256 * 32;   // slots per compaction tile (256 threads x one 32-slot word)
+
+// occupancy bitmap of an interval whose claims did not set it (the direct form): slot s is
+// occupied iff its tag carries the interval's epoch.  One lane per 32-slot word; the tags
+// are 8-byte loads at the record stride.
+__global__ __launch_bounds__(256) void k_occ_from_tags(const uint8_t *__restrict__ krec, uint32_t krec_len,
+                                                       uint32_t koff, uint64_t ns, uint64_t ep,
+                                                       uint32_t *__restrict__ occ) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w * 32 >= ns) return;
+    uint32_t m = 0;
+#pragma unroll 8
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint64_t s = w * 32 + b;
+        const uint64_t t = s < ns ? *reinterpret_cast<const uint64_t *>(krec + s * krec_len + koff) : 0;
+        m |= ((t & EP_MAX) == ep ? 1u : 0u) << b;
+    }
+    occ[w] |= m;   // OR: earlier cached updates of the interval may have set bits already
+}
 
 __global__ __launch_bounds__(256) void k_slots_count(const uint32_t *__restrict__ occ, uint64_t nwords,
                                                      uint32_t *__restrict__ cnt) {
@@ -1259,6 +1334,9 @@ struct igx_table {
     uint64_t *n_groups = nullptr;
     uint64_t rows_fed = 0;       // rows given to update since the last reset
     bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
+    uint32_t mode = IGX_GB_AUTO; // igx_groupby_set_mode
+    uint32_t direct_left = 0;    // AUTO: intervals to run in the direct form before re-measuring
+    bool interval_direct = false;// the current interval's updates run the direct form
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[8] = {};       // IP text of the groups, per IGX_TSRC_IPTEXT sort key
@@ -1406,6 +1484,8 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
 }
 
 constexpr size_t GB_LDS_TOTAL = 156 * 1024;    // cache + the two rings (dynamic LDS)
+constexpr uint64_t DIRECT_MISS_PCT = 90;        // AUTO: LDS-miss share that selects the direct form
+constexpr uint32_t DIRECT_RUN = 16;             // ... for this many intervals
 
 template <class L, bool DBG, int NA>
 static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
@@ -1438,6 +1518,45 @@ static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     }
     if (a.naggs <= 2) launch_gb_as<L, false, 2>(ctx, a, blocks);
     else launch_gb_as<L, false, AMAX>(ctx, a, blocks);
+}
+
+// The grid is exactly the blocks that are resident at once (the occupancy the kernel's
+// registers allow): every block sweeps a fixed share of the rows, so a block that had to wait
+// for a free slot would run its whole share after the others -- a tail of up to 1/8 of the time.
+template <class L, int NA>
+static void launch_direct_as(igx_ctx *ctx, GbArgs &a) {
+    static int per_cu = 0;
+    if (!per_cu) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void *>(k_groupby_direct<L, NA>),
+                                                         256, 0) != hipSuccess || b < 1)
+            b = 4;
+        per_cu = std::min(b, 8);
+    }
+    const uint64_t want = (a.n + 255) / 256;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus * per_cu));
+    hipLaunchKernelGGL((k_groupby_direct<L, NA>), dim3(blocks), dim3(256), 0, ctx->stream, a);
+}
+
+template <class L>
+static void launch_direct(igx_ctx *ctx, GbArgs &a) {
+    if (a.naggs <= 2) launch_direct_as<L, 2>(ctx, a);
+    else launch_direct_as<L, AMAX>(ctx, a);
+}
+
+// one update over layout L in the interval's form
+template <class L>
+static void launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+    if (t->interval_direct) launch_direct<L>(ctx, a);
+    else launch_gb<L>(ctx, a, blocks);
+}
+
+extern "C" int igx_groupby_set_mode(igx_table *t, uint32_t mode) {
+    if (!t) return IGX_EINVAL;
+    if (mode > IGX_GB_DIRECT) return igx_fail(t->ctx, IGX_EINVAL, "groupby_set_mode: mode %u", mode);
+    t->mode = mode;
+    t->direct_left = 0;
+    return IGX_OK;
 }
 
 extern "C" int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols, const uint32_t *key_cols,
@@ -1614,28 +1733,35 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     const uint64_t want = (nrows + GTB - 1) / GTB;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus));
     const uint32_t *kw = t->key_widths;
+    // the interval's form is fixed by its first update (the LDS-miss count that drives AUTO
+    // is only meaningful for a whole interval of the cached form)
+    if (t->rows_fed == nrows) {
+        t->interval_direct = t->mode == IGX_GB_DIRECT || (t->mode == IGX_GB_AUTO && t->direct_left > 0);
+        if (t->mode == IGX_GB_AUTO && t->direct_left > 0) --t->direct_left;
+    }
+    if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = false;   // diagnostics run the cached form
     if (t->generic) {
         switch (t->kw_rec) {
-        case 2: launch_gb<GenericLayout<2>>(ctx, a, blocks); break;
-        case 4: launch_gb<GenericLayout<4>>(ctx, a, blocks); break;
-        case 6: launch_gb<GenericLayout<6>>(ctx, a, blocks); break;
-        case 8: launch_gb<GenericLayout<8>>(ctx, a, blocks); break;
-        case 12: launch_gb<GenericLayout<12>>(ctx, a, blocks); break;
-        case 18: launch_gb<GenericLayout<18>>(ctx, a, blocks); break;
-        case 24: launch_gb<GenericLayout<24>>(ctx, a, blocks); break;
-        case 32: launch_gb<GenericLayout<32>>(ctx, a, blocks); break;
+        case 2: launch_form<GenericLayout<2>>(t, ctx, a, blocks); break;
+        case 4: launch_form<GenericLayout<4>>(t, ctx, a, blocks); break;
+        case 6: launch_form<GenericLayout<6>>(t, ctx, a, blocks); break;
+        case 8: launch_form<GenericLayout<8>>(t, ctx, a, blocks); break;
+        case 12: launch_form<GenericLayout<12>>(t, ctx, a, blocks); break;
+        case 18: launch_form<GenericLayout<18>>(t, ctx, a, blocks); break;
+        case 24: launch_form<GenericLayout<24>>(t, ctx, a, blocks); break;
+        case 32: launch_form<GenericLayout<32>>(t, ctx, a, blocks); break;
         default: return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: no kernel for %u key words", t->kw_rec);
         }
-    } else if (layout_is<TcpKey>(kw, t->nkeys)) launch_gb<TcpKey>(ctx, a, blocks);
-    else if (layout_is<FileKey>(kw, t->nkeys)) launch_gb<FileKey>(ctx, a, blocks);
+    } else if (layout_is<TcpKey>(kw, t->nkeys)) launch_form<TcpKey>(t, ctx, a, blocks);
+    else if (layout_is<FileKey>(kw, t->nkeys)) launch_form<FileKey>(t, ctx, a, blocks);
     else if (layout_is<NetPolicyKey>(kw, t->nkeys))
-        launch_gb<NetPolicyKey>(ctx, a, blocks);
-    else if (layout_is<BioKey>(kw, t->nkeys)) launch_gb<BioKey>(ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 1) launch_gb<StaticLayout<1>>(ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 2) launch_gb<StaticLayout<2>>(ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 4) launch_gb<StaticLayout<4>>(ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 8) launch_gb<StaticLayout<8>>(ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 16) launch_gb<StaticLayout<16>>(ctx, a, blocks);
+        launch_form<NetPolicyKey>(t, ctx, a, blocks);
+    else if (layout_is<BioKey>(kw, t->nkeys)) launch_form<BioKey>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 1) launch_form<StaticLayout<1>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 2) launch_form<StaticLayout<2>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 4) launch_form<StaticLayout<4>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 8) launch_form<StaticLayout<8>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 16) launch_form<StaticLayout<16>>(t, ctx, a, blocks);
     else return igx_fail(ctx, IGX_EINVAL, "groupby_update: internal layout mismatch");
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
@@ -1645,6 +1771,9 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     const uint64_t tiles = (t->nslots + CT - 1) / CT;
+    if (t->interval_direct)
+        hipLaunchKernelGGL(k_occ_from_tags, dim3((unsigned)((t->occ_words + 255) / 256)), dim3(256), 0, ctx->stream,
+                           t->krec, t->krec_len, t->koff, t->nslots, t->ep, t->occ);
     hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                        t->tile_cnt);
     hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups);
@@ -1662,8 +1791,13 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     const uint64_t misses = h[2];
     t->host_groups = ng;
     // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
-    // go faster with the state-machine probers; hit-heavy ones with the batch probers.
-    if (t->rows_fed >= 1000000) t->prefer_sm = misses * 10 > t->rows_fed * 7;
+    // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When
+    // nearly every row missed, the cache is pure overhead: AUTO runs the next DIRECT_RUN
+    // intervals in the direct form, then one cached interval to measure again.
+    if (t->rows_fed >= 1000000 && !t->interval_direct) {
+        t->prefer_sm = misses * 10 > t->rows_fed * 7;
+        if (t->mode == IGX_GB_AUTO && misses * 100 > t->rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
+    }
     if (view) {
         view->n_groups = ng;
         view->n_slots = t->nslots;

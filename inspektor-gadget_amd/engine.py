@@ -217,6 +217,10 @@ class Table:
     def reset(self):
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
 
+    def set_mode(self, mode):
+        """igx_groupby_set_mode: _abi.GB_AUTO (default), GB_CACHED or GB_DIRECT."""
+        self.ctx.check(self.ctx.L.igx_groupby_set_mode(self.h, mode))
+
     def finalize(self):
         """Synchronises.  Returns the table view (raw device pointers, slot-indexed) as a
         dict; `groups_ptr` lists the n_groups occupied slots."""
