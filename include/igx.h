@@ -266,7 +266,9 @@ int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys,
                        igx_table **out);
 /* Aggregate rows [0,nrows) of cols into the table; key_cols selects the key columns
  * (in the table's key order); preds are AND-ed filters applied first (the BPF probe
- * checks).  base_idx is the global index of row 0 (first-occurrence order).  Async. */
+ * checks).  base_idx is the global index of row 0 (first-occurrence order); indices must
+ * stay below 2^48 - 1 (IGX_EINVAL otherwise; an index column value at or above it fails the
+ * interval at finalize): long-running streams rebase their indices per interval.  Async. */
 int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols,
                        const uint32_t *key_cols, const igx_pred *preds, uint32_t npreds,
                        uint64_t nrows, uint64_t base_idx);

@@ -100,6 +100,7 @@ extern "C" int igx_close(igx_ctx *ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     for (auto &r : ctx->regex) (void)hipFree(r.second);
+    if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
     return IGX_OK;
@@ -109,7 +110,16 @@ extern "C" const char *igx_last_error(igx_ctx *ctx) { return ctx ? ctx->err.c_st
 
 extern "C" int igx_set_stream(igx_ctx *ctx, void *s) {
     if (!ctx) return IGX_EINVAL;
-    ctx->stream = static_cast<hipStream_t>(s);
+    hipStream_t ns = static_cast<hipStream_t>(s);
+    if (ns != ctx->stream && ctx->scratch) {
+        // the scratch arena (and the pinned staging) belong to the context, not to a stream: work
+        // enqueued next on the new stream waits for what the old stream still has in flight, so
+        // two calls on different streams never share the arena concurrently
+        if (!ctx->handoff) IGX_HIP(ctx, hipEventCreateWithFlags(&ctx->handoff, hipEventDisableTiming));
+        IGX_HIP(ctx, hipEventRecord(ctx->handoff, ctx->stream));
+        IGX_HIP(ctx, hipStreamWaitEvent(ns, ctx->handoff, 0));
+    }
+    ctx->stream = ns;
     return IGX_OK;
 }
 

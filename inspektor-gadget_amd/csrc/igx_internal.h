@@ -25,6 +25,8 @@ struct igx_ctx {
     size_t pinned_bytes = 0;
     // compiled regex automata on the device, by pattern (freed by igx_close)
     std::map<std::string, void *> regex;
+    // igx_set_stream: the new stream waits on this event recorded on the old one
+    hipEvent_t handoff = nullptr;
 };
 
 // sets ctx->err and returns code

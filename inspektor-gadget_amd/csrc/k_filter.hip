@@ -172,8 +172,8 @@ __device__ __forceinline__ void take_copy(const uint8_t *s, uint8_t *d, uint32_t
 }
 
 __global__ __launch_bounds__(TB) void k_take(TakeArgs a, const uint32_t *__restrict__ idx, uint64_t k,
-                                             uint64_t nrows) {
-    const uint64_t r = (uint64_t)blockIdx.x * TB + threadIdx.x;
+                                             uint64_t nrows, uint64_t r0) {
+    const uint64_t r = r0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
     if (r >= k) return;
     const uint32_t c = blockIdx.y;
     const uint32_t width = a.width[c];
@@ -197,7 +197,7 @@ extern "C" int igx_take(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, uint6
     if (!ctx) return IGX_EINVAL;
     if (k == 0 || ncols == 0) return IGX_OK;
     if (!cols || !idx || !out) return igx_fail(ctx, IGX_EINVAL, "take: null argument");
-    if (k >= (1ull << 32) * TB) return igx_fail(ctx, IGX_EINVAL, "take: too many rows");
+
     for (uint32_t c0 = 0; c0 < ncols; c0 += TAKE_MAXC) {
         const uint32_t nc = ncols - c0 < TAKE_MAXC ? ncols - c0 : TAKE_MAXC;
         TakeArgs a{};
@@ -211,8 +211,13 @@ extern "C" int igx_take(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, uint6
             const uint64_t al = (uint64_t)(uintptr_t)col.ptr | (uint64_t)(uintptr_t)out[c0 + j] | col.width;
             a.unit[j] = (al & 15) == 0 ? 16 : (al & 7) == 0 ? 8 : (al & 3) == 0 ? 4 : (al & 1) == 0 ? 2 : 1;
         }
-        hipLaunchKernelGGL(k_take, dim3((unsigned)((k + TB - 1) / TB), nc), dim3(TB), 0, ctx->stream, a, idx, k,
-                           nrows);
+        // at most 2^20 blocks per launch (a grid dimension is capped at 2^32 - 1 work-items)
+        constexpr uint64_t ROWS = (1ull << 20) * TB;
+        for (uint64_t r0 = 0; r0 < k; r0 += ROWS) {
+            const uint64_t m = std::min<uint64_t>(ROWS, k - r0);
+            hipLaunchKernelGGL(k_take, dim3((unsigned)((m + TB - 1) / TB), nc), dim3(TB), 0, ctx->stream, a, idx, k,
+                               nrows, r0);
+        }
     }
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;

@@ -315,6 +315,10 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
         uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
         uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
         if ((t & EP_MAX) != a.ep) {   // empty in this interval (never claimed, or an older epoch's)
+            if (gidx >= READY_IDX) {   // an index column value that `ready` cannot carry
+                atomicOr(a.err, 8u);
+                return SLOT_OVF;
+            }
             const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(r + KOFF),
                                            (unsigned long long)t, (unsigned long long)tag);
             if (old == t) {
@@ -1572,6 +1576,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     if (nrows == 0) return IGX_OK;
     if (!cols || !key_cols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: null columns");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "groupby_update: more than 2^32 rows in one call");
+    if (base_idx + nrows > READY_IDX)   // `ready` carries first_ins + 1 in 48 bits
+        return igx_fail(ctx, IGX_EINVAL, "groupby_update: event indices reach 2^48 (rebase the interval's indices)");
     t->rows_fed += nrows;
     GbArgs a{};
     uint32_t w = 0;

@@ -252,6 +252,10 @@ _ENRICH = {"node": ("const",), "namespace": ("const",), "pod": ("const",), "cont
 @dataclass
 class TcpStats:
     """pkg/gadgets/top/tcp/types/types.go:46-58."""
+    Node: str = ""           # eventtypes.CommonData (pkg/types/types.go:73-87), filled by enrichers
+    Namespace: str = ""
+    Pod: str = ""
+    Container: str = ""
     MountNsID: int = 0
     Pid: int = 0
     Comm: str = ""
@@ -324,6 +328,10 @@ class TopTcpTracer(_TopTracer):
 @dataclass
 class FileStats:
     """pkg/gadgets/top/file/types/types.go:37-51."""
+    Node: str = ""           # eventtypes.CommonData (pkg/types/types.go:73-87), filled by enrichers
+    Namespace: str = ""
+    Pod: str = ""
+    Container: str = ""
     MountNsID: int = 0
     Pid: int = 0
     Tid: int = 0
@@ -397,6 +405,10 @@ class TopFileTracer(_TopTracer):
 @dataclass
 class BlockIOStats:
     """pkg/gadgets/top/block-io/types/types.go:35-48."""
+    Node: str = ""           # eventtypes.CommonData (pkg/types/types.go:73-87), filled by enrichers
+    Namespace: str = ""
+    Pod: str = ""
+    Container: str = ""
     MountNsID: int = 0
     Pid: int = 0
     Comm: str = ""
@@ -439,6 +451,105 @@ class TopBlockIOTracer(_TopTracer):
                                     Bytes=int(nbytes[i]), MicroSecs=int(us[i]),
                                     Operations=int(io[i]) & 0xFFFFFFFF, FirstIndex=int(first[i])))
         return out
+
+
+# ------------------------------------------------------------------------------------
+# output side: the Stats types' column tags and JSON fields
+# ------------------------------------------------------------------------------------
+# eventtypes.CommonData + WithMountNsID (pkg/types/types.go:73-87,217-219)
+_COMMON_COLS = [("Node", "string", "node,template:node", ["kubernetes"]),
+                ("Namespace", "string", "namespace,template:namespace", ["kubernetes"]),
+                ("Pod", "string", "pod,template:pod", ["kubernetes"]),
+                ("Container", "string", "container,template:container", ["kubernetes", "runtime"]),
+                ("MountNsID", "uint64", "mntns,template:ns", [])]
+_COMMON_JSON = [("Node", "node", True), ("Namespace", "namespace", True), ("Pod", "pod", True),
+                ("Container", "container", True), ("MountNsID", "mountnsid", True)]
+
+STATS_OUTPUT = {
+    # pkg/gadgets/top/tcp/types/types.go:46-101
+    "tcp": {
+        "fields": _COMMON_COLS + [("Pid", "int32", "pid,template:pid", []), ("Comm", "string", "comm,template:comm", []),
+                                  ("Family", "uint16", "ip,maxWidth:2", []),
+                                  ("Saddr", "string", "saddr,template:ipaddr,hide", []),
+                                  ("Daddr", "string", "daddr,template:ipaddr,hide", []),
+                                  ("Sport", "uint16", "sport,template:ipport,hide", []),
+                                  ("Dport", "uint16", "dport,template:ipport,hide", []),
+                                  ("Sent", "uint64", "sent,order:1002", []),
+                                  ("Received", "uint64", "recv,order:1003", [])],
+        "json": _COMMON_JSON + [("Pid", "pid", True), ("Comm", "comm", True), ("Family", "family", True),
+                                ("Saddr", "saddr", True), ("Daddr", "daddr", True), ("Sport", "sport", True),
+                                ("Dport", "dport", True), ("Sent", "sent", True), ("Received", "received", True)],
+    },
+    # pkg/gadgets/top/file/types/types.go:37-66
+    "file": {
+        "fields": _COMMON_COLS + [("Pid", "uint32", "pid,template:pid", []), ("Tid", "uint32", "tid,template:pid,hide", []),
+                                  ("Comm", "string", "comm,template:comm", []), ("Reads", "uint64", "reads", []),
+                                  ("Writes", "uint64", "writes", []), ("ReadBytes", "uint64", "rbytes", []),
+                                  ("WriteBytes", "uint64", "wbytes", []), ("FileType", "uint8", "T,maxWidth:1", []),
+                                  ("Filename", "string", "file", [])],
+        "json": _COMMON_JSON + [("Pid", "pid", True), ("Tid", "tid", True), ("Comm", "comm", True),
+                                ("Reads", "reads", True), ("Writes", "writes", True), ("ReadBytes", "rbytes", True),
+                                ("WriteBytes", "wbytes", True), ("FileType", "fileType", True),
+                                ("Filename", "filename", True)],
+    },
+    # pkg/gadgets/top/block-io/types/types.go:34-61
+    "block-io": {
+        "fields": _COMMON_COLS + [("Pid", "int32", "pid", []), ("Comm", "string", "comm", []),
+                                  ("Write", "bool", "r/w,maxWidth:3", []), ("Major", "int", "major", []),
+                                  ("Minor", "int", "minor", []), ("Bytes", "uint64", "bytes", []),
+                                  ("MicroSecs", "uint64", "time", []), ("Operations", "uint32", "ops", [])],
+        "json": _COMMON_JSON + [("Pid", "pid", True), ("Comm", "comm", True), ("Write", "write", True),
+                                ("Major", "major", True), ("Minor", "minor", True), ("Bytes", "bytes", True),
+                                ("MicroSecs", "us", True), ("Operations", "ops", True)],
+    },
+}
+
+
+def StatsColumns(gadget: str):
+    """types.GetColumns() of a top gadget's Stats: the tagged fields plus its extractors and
+    virtual columns, as a textcolumns.ColumnMap (every column; see OutputColumns for the
+    frontends' tag filter)."""
+    from . import textcolumns as T
+    spec = STATS_OUTPUT[gadget]
+    cm = T.ColumnMap([(attr, kind, tag) for attr, kind, tag, _ in spec["fields"]])
+    for attr, kind, tag, tags in spec["fields"]:
+        cm.cols[tag.split(",")[0].lower()].Tags = list(tags)
+    if gadget == "tcp":
+        cm.SetExtractor("ip", lambda st: "4" if st.Family == AF_INET else "6")
+        cm.SetExtractor("sent", lambda st: T.BytesSize(float(st.Sent)))
+        cm.SetExtractor("recv", lambda st: T.BytesSize(float(st.Received)))
+        cm.AddColumn("local", lambda st: f"{st.Saddr}:{st.Sport}", MinWidth=21, MaxWidth=51, Order=1000)
+        cm.AddColumn("remote", lambda st: f"{st.Daddr}:{st.Dport}", MinWidth=21, MaxWidth=51, Order=1000)
+    elif gadget == "file":
+        cm.SetExtractor("rbytes", lambda st: T.BytesSize(float(st.ReadBytes)))
+        cm.SetExtractor("wbytes", lambda st: T.BytesSize(float(st.WriteBytes)))
+        cm.SetExtractor("T", lambda st: chr(st.FileType))
+    else:
+        cm.SetExtractor("r/w", lambda st: "W" if st.Write else "R")
+    return cm
+
+
+def OutputColumns(gadget: str, metadata_tag: str = ""):
+    """The column map a frontend formats with (parser-tableformatter.go:60-65): columns
+    without tags, plus those carrying metadata_tag ("kubernetes" for kubectl-gadget, "runtime"
+    for ig with a container runtime; "" = untagged only)."""
+    cm = StatsColumns(gadget)
+    cm.cols = {k: c for k, c in cm.cols.items() if not c.Tags or (metadata_tag and metadata_tag in c.Tags)}
+    return cm
+
+
+def render_table(gadget: str, stats, metadata_tag: str = "", terminal_width: int = 0, columns=None) -> str:
+    """The columns output of one interval (GadgetParser.TransformIntoTable over the interval's
+    []*Stats, cmd/common/utils/parser-tableformatter.go:106-111)."""
+    from . import textcolumns as T
+    f = T.TextColumnsFormatter(OutputColumns(gadget, metadata_tag), DefaultColumns=columns)
+    return T.TransformIntoTable(f, stats, terminal_width)
+
+
+def render_json(gadget: str, stats) -> str:
+    """-o json: json.Marshal of the interval's []*Stats (cmd/common/registry.go:511-520)."""
+    from . import textcolumns as T
+    return T.marshal_array(stats, STATS_OUTPUT[gadget]["json"])
 
 
 def rwflag_of(cmd_flags):

@@ -11,6 +11,8 @@ Produces data only (inputs + expected outputs), never reference source:
                          :46-124 (values only) and the multi-filter case :287-298.
 * advisor/*.input/.golden -- pkg/gadgets/advise/networkpolicy/advisor/testdata (data files
                          the reference's own golden test uses, advisor_test.go:23-51).
+* ellipsis_table.json -- the (Input, MaxLength, Type, Result) rows of
+                         pkg/columns/ellipsis/ellipsis_test.go:21-206.
 
 The group_test.go and sort_test.go expectations are small enough that they are written
 out by hand in tests/test_oracle_golden.py, each with its file:line.
@@ -52,6 +54,19 @@ def main(ref):
     for fn in sorted(os.listdir(adv_src)):
         shutil.copy(os.path.join(adv_src, fn), os.path.join(adv_dst, fn))
     print(f"{len(table)} filter rows, {len(os.listdir(adv_dst))} advisor files")
+    ellipsis_table(ref, here)
+
+
+def ellipsis_table(ref, here):
+    src = open(os.path.join(ref, "pkg/columns/ellipsis/ellipsis_test.go")).read()
+    rows = re.findall(r'Input:\s+"((?:[^"\\]|\\.)*)",\s*MaxLength:\s+(\d+),\s*Type:\s+(\w+),\s*'
+                      r'Result:\s+"((?:[^"\\]|\\.)*)"', src)
+    out = {"source": "pkg/columns/ellipsis/ellipsis_test.go:21-206",
+           "rows": [{"input": json.loads('"' + i + '"'), "max": int(m), "type": t,
+                     "result": json.loads('"' + r + '"')} for i, m, t, r in rows]}
+    with open(os.path.join(here, "ellipsis_table.json"), "w") as fh:
+        json.dump(out, fh, indent=1, ensure_ascii=False)
+    return len(rows)
 
 
 if __name__ == "__main__":
