@@ -14,7 +14,7 @@ from ._abi import IgxError, lib  # noqa: F401  (loads libigx.so eagerly: fail lo
 lib()
 
 from . import runtime, engine  # noqa: E402,F401
-from . import columns, filter, sort, group, top, dist, advisor, gadgets, parser, wire, textcolumns  # noqa: E402,F401
+from . import columns, filter, sort, group, top, dist, advisor, gadgets, parser, wire, textcolumns, operators  # noqa: E402,F401
 
 __all__ = ["IgxError", "lib", "runtime", "engine", "columns", "filter", "sort", "group", "top",
-           "dist", "advisor", "gadgets", "parser", "wire", "textcolumns"]
+           "dist", "advisor", "gadgets", "parser", "wire", "textcolumns", "operators"]
