@@ -296,10 +296,13 @@ int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete lo
  *                  most rows never leave the CU);
  *   IGX_GB_DIRECT  every row probes the HBM table itself (near-uniform, high-cardinality
  *                  streams, where nearly every row would miss the cache);
+ *   IGX_GB_PART    rows are radix-partitioned by key hash in two streamed passes and each
+ *                  final bucket is aggregated in LDS, then written to the table with plain
+ *                  stores (no atomics; DESIGN.md §4 has its measured cost);
  *   IGX_GB_AUTO    (default) cached; an interval in which more than 90% of the rows missed
  *                  the cache switches the next 16 intervals to direct, then measures again.
  * The mode of an interval is fixed by its first update. */
-enum igx_gb_mode { IGX_GB_AUTO = 0, IGX_GB_CACHED = 1, IGX_GB_DIRECT = 2 };
+enum igx_gb_mode { IGX_GB_AUTO = 0, IGX_GB_CACHED = 1, IGX_GB_DIRECT = 2, IGX_GB_PART = 3 };
 int igx_groupby_set_mode(igx_table *t, uint32_t mode);
 /* SortStats over the table's groups (same order as igx_sort_perm with pos = first_idx);
  * writes the first k (0 = all) group slots to out_slots (device u32).  Call after

@@ -24,7 +24,7 @@ NO_COL = 0xFFFFFFFF
 MAX_REF = 256
 AGG_COUNT, AGG_SUM = 0, 1
 FILTER_ANY, FILTER_NIL_MATCH = 1, 2
-GB_AUTO, GB_CACHED, GB_DIRECT = 0, 1, 2
+GB_AUTO, GB_CACHED, GB_DIRECT, GB_PART = 0, 1, 2, 3
 
 
 class SchemaCol(C.Structure):
@@ -159,6 +159,11 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                               "(or `make -C inspektor-gadget_amd/csrc`)")
+        # torch bundles its own libamdhip64 / libhsa-runtime64 / librccl under the same
+        # sonames as /opt/rocm's.  Whichever loads first serves the process, so torch goes
+        # first: libigx.so loaded before it pulls in /opt/rocm's runtime, and torch on top
+        # of that runtime leaves hipGetDeviceCount failing inside libigx (igx_open ENOENT).
+        import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)

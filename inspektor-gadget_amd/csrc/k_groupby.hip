@@ -118,7 +118,8 @@ struct GbArgs {
     uint32_t *occ;          // occupancy bitmap, one bit per slot (set by the claimer)
     uint64_t ep;            // the interval's epoch (1..EP_MAX): tags and `ready` of older
                             // epochs read as empty
-    uint64_t mask;
+    uint64_t rmask;         // probe region slots - 1 (probing wraps inside a region)
+    uint32_t sshift;        // home slot = h >> sshift (the hash's top bits)
     uint32_t max_probe;
     // diagnostics (IGX_GB_DEBUG; compiled into the top-tcp key's debug kernel only):
     // bit0 stop after load+hash, bit1 drop LDS misses, bit10 probers drop the cells they take, bit2 drop HBM atomics, bit3 count
@@ -270,6 +271,14 @@ __device__ __forceinline__ bool pred_scalar(uint64_t v, uint64_t ref, uint32_t w
     return r != (neg != 0);
 }
 
+// A key's home slot is the hash's top bits and linear probing wraps inside the slot's
+// region (table.rbits): a bucket of the partitioned form (also the hash's top bits) then owns
+// whole regions of the table, in every form alike.
+__device__ __forceinline__ uint64_t home_slot(const GbArgs &a, uint64_t h) { return h >> a.sshift; }
+__device__ __forceinline__ uint64_t next_slot(const GbArgs &a, uint64_t s) {
+    return (s & ~a.rmask) | ((s + 1) & a.rmask);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const GbArgs &a) {
     return __builtin_amdgcn_make_buffer_rsrc(a.krec, (short)0, (int)a.krec_total, 0x00020000);
 }
@@ -295,7 +304,7 @@ constexpr int probe_quads() { return (int)((koff_of(KW) + 16 + 15) / 16); }   //
 // the home slot's record, issued early so its round trip overlaps other work
 template <int KW>
 __device__ __forceinline__ void probe_issue(const GbArgs &a, uint64_t h, uint32_t (&d)[probe_quads<KW>() * 4]) {
-    load_rec<probe_quads<KW>()>(rec_rsrc(a), (uint32_t)(((h >> 17) & a.mask) * a.krec_len), d);
+    load_rec<probe_quads<KW>()>(rec_rsrc(a), (uint32_t)(home_slot(a, h) * a.krec_len), d);
 }
 
 // d holds the home slot's record (probe_issue)
@@ -307,7 +316,7 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
     constexpr int NQ = probe_quads<KW>();
     const uint64_t tag = (h & ~EP_MAX) | a.ep;
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
-    uint64_t s = (h >> 17) & a.mask;
+    uint64_t s = home_slot(a, h);
     for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
         const uint32_t off = (uint32_t)(s * a.krec_len);
         if (probe) load_rec<NQ>(rs, off, d);
@@ -377,7 +386,7 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                 return (uint32_t)s;
             }
         }
-        s = (s + 1) & a.mask;
+        s = next_slot(a, s);
     }
     atomicOr(a.err, 4u);
     return SLOT_OVF;
@@ -467,25 +476,51 @@ __device__ __forceinline__ void issue_row(const GbArgs &a, uint64_t row, RowRaw<
     }
 }
 
-template <class L, int NA>
-__device__ __forceinline__ bool decode_row(const GbArgs &a, uint64_t row, const RowRaw<L, NA> &R,
-                                           uint32_t (&k)[L::KW], uint64_t (&v)[NA]) {
-#pragma unroll
-    for (int w = 0; w < L::KW; ++w) k[w] = R.k[w];
-    uint32_t vlo[NA], vhi[NA], clo[NA], chi[NA];
-#pragma unroll
-    for (int x = 0; x < NA; ++x) {
-        vlo[x] = R.vlo[x]; vhi[x] = R.vhi[x]; clo[x] = R.clo[x]; chi[x] = R.chi[x];
-    }
-    // aggregates reading a column an earlier one already loaded reuse its dwords
+// aggregates reading a column an earlier one already loaded reuse its value
+template <int NA>
+__device__ __forceinline__ void share_raw(const GbArgs &a, uint64_t (&rv)[NA], uint64_t (&rc)[NA]) {
 #pragma unroll
     for (int x = 1; x < NA; ++x) {
 #pragma unroll
         for (int y = 0; y < x; ++y) {
-            if (a.vshare[x] == (uint32_t)y) { vlo[x] = vlo[y]; vhi[x] = vhi[y]; }
-            if (a.cshare[x] == (uint32_t)y) { clo[x] = clo[y]; chi[x] = chi[y]; }
+            if (a.vshare[x] == (uint32_t)y) rv[x] = rv[y];
+            if (a.cshare[x] == (uint32_t)y) rc[x] = rc[y];
         }
     }
+}
+
+// the value each aggregate adds: 1 (COUNT) or the column's value (sign-extended, divided),
+// 0 when its condition column does not hold cval
+template <int NA>
+__device__ __forceinline__ void vals_from_raw(const GbArgs &a, const uint64_t (&rv)[NA], const uint64_t (&rc)[NA],
+                                              uint64_t (&v)[NA]) {
+#pragma unroll
+    for (int x = 0; x < NA; ++x) {
+        uint64_t val = 0;
+        if (x < (int)a.naggs) {
+            val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(rv[x], a.vwidth[x]) : rv[x]);
+            if (a.vdiv[x]) val /= a.vdiv[x];
+            if (a.hascond[x] && rc[x] != a.cval[x]) val = 0;
+        }
+        v[x] = val;
+    }
+}
+
+// A row's key words, whether it is kept (valid and predicates), and the zero-extended raw
+// value / condition column values of its aggregates (an aggregate that shares another's
+// column takes that one's value).  vals_from_raw turns them into the added values; the
+// partitioned form stores the raw values of the loaded columns in its records.
+template <class L, int NA>
+__device__ __forceinline__ bool row_raw(const GbArgs &a, uint64_t row, const RowRaw<L, NA> &R,
+                                        uint32_t (&k)[L::KW], uint64_t (&rv)[NA], uint64_t (&rc)[NA]) {
+#pragma unroll
+    for (int w = 0; w < L::KW; ++w) k[w] = R.k[w];
+#pragma unroll
+    for (int x = 0; x < NA; ++x) {
+        rv[x] = assemble(R.vlo[x], R.vhi[x], row * a.vwidth[x], a.vwidth[x]);
+        rc[x] = assemble(R.clo[x], R.chi[x], row * a.cwidth[x], a.cwidth[x]);
+    }
+    share_raw<NA>(a, rv, rc);
     bool ok = !a.valid || ((R.vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
@@ -494,18 +529,15 @@ __device__ __forceinline__ bool decode_row(const GbArgs &a, uint64_t row, const 
             ok = ok && pred_scalar(pv, a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p], a.pcnt[p]);
         }
     }
-#pragma unroll
-    for (int x = 0; x < NA; ++x) {
-        uint64_t val = 0;
-        if (x < (int)a.naggs) {
-            const uint64_t raw = assemble(vlo[x], vhi[x], row * a.vwidth[x], a.vwidth[x]);
-            const uint64_t cv = assemble(clo[x], chi[x], row * a.cwidth[x], a.cwidth[x]);
-            val = a.vcount[x] ? 1ull : (a.vsign[x] ? sext(raw, a.vwidth[x]) : raw);
-            if (a.vdiv[x]) val /= a.vdiv[x];
-            if (a.hascond[x] && cv != a.cval[x]) val = 0;
-        }
-        v[x] = val;
-    }
+    return ok;
+}
+
+template <class L, int NA>
+__device__ __forceinline__ bool decode_row(const GbArgs &a, uint64_t row, const RowRaw<L, NA> &R,
+                                           uint32_t (&k)[L::KW], uint64_t (&v)[NA]) {
+    uint64_t rv[NA], rc[NA];
+    const bool ok = row_raw<L, NA>(a, row, R, k, rv, rc);
+    vals_from_raw<NA>(a, rv, rc, v);
     return ok;
 }
 
@@ -884,7 +916,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
                             lds_accumulate<KW, NA>(a, c, slot, x.v, x.gidx);
                         } else {
                             st = PROBE;
-                            s = (uint32_t)((x.h >> 17) & a.mask);
+                            s = (uint32_t)home_slot(a, x.h);
                             probes = 0;
                             tries = 0;
                             reread = 0;
@@ -940,7 +972,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
             } else {
                 st = PROBE;   // lost to another key (the CAS saw the current tag): next slot
                 reread = 0;
-                s = (uint32_t)((s + 1) & a.mask);
+                s = (uint32_t)next_slot(a, s);
                 if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
             }
         }
@@ -967,13 +999,13 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
                         ++tries;
                     } else {
                         reread = 0;
-                        s = (uint32_t)((s + 1) & a.mask);
+                        s = (uint32_t)next_slot(a, s);
                         if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
                     }
                 }
             } else {
                 reread = 0;
-                s = (uint32_t)((s + 1) & a.mask);
+                s = (uint32_t)next_slot(a, s);
                 if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
             }
         }
@@ -1037,7 +1069,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
             if (probe[j]) {
                 uint64_t first_ins = 0;
                 uint32_t gs;
-                if (DBG && (a.dbg & 256u)) gs = (uint32_t)((x[j].h >> 17) & a.mask);   // diagnostics: no probe
+                if (DBG && (a.dbg & 256u)) gs = (uint32_t)home_slot(a, x[j].h);   // diagnostics: no probe
                 else gs = find_or_insert<KW>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j]);
                 if (gs != SLOT_OVF) {
                     const int ad = ghost_admit<KW>(a, c, x[j].h) ? lds_adopt<KW>(c, x[j].k, x[j].h, gs) : -1;
@@ -1310,6 +1342,8 @@ __global__ void k_gather_rows(const uint8_t *__restrict__ krec, uint32_t krec_le
     }
 }
 
+#include "k_groupby_part.h"
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -1327,6 +1361,8 @@ struct igx_table {
     uint32_t naggs = 0;
     uint64_t cap = 0;            // distinct keys promised by the caller
     uint64_t nslots = 0;
+    uint32_t sbits = 0;          // log2 nslots
+    uint32_t rbits = 0;          // log2 probe-region slots (probing wraps inside a region)
     uint8_t *krec = nullptr;
     uint64_t *vrec = nullptr;
     uint32_t *err = nullptr;
@@ -1341,6 +1377,12 @@ struct igx_table {
     uint32_t mode = IGX_GB_AUTO; // igx_groupby_set_mode
     uint32_t direct_left = 0;    // AUTO: intervals to run in the direct form before re-measuring
     bool interval_direct = false;// the current interval's updates run the direct form
+    bool interval_part = false;  // ... the partitioned form
+    // partitioned form scratch (grow-only)
+    uint32_t *p_recs = nullptr;
+    size_t p_recs_bytes = 0;
+    uint32_t *p_cnt = nullptr;   // counts / offsets, then scan tile sums, then work items
+    size_t p_cnt_bytes = 0;
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[8] = {};       // IP text of the groups, per IGX_TSRC_IPTEXT sort key
@@ -1427,6 +1469,10 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     uint64_t ns = 1024;
     while (ns * 4 < slotf * capacity) ns <<= 1;
     t->nslots = ns;
+    t->sbits = (uint32_t)__builtin_ctzll(ns);
+    // probe regions of max(1024, S / 16384) slots: up to 16K regions, so a bucket of the
+    // partitioned form can own whole regions
+    t->rbits = std::max<uint32_t>(10, t->sbits > 14 ? t->sbits - 14 : 0);
     if (ns * t->krec_len >= (1ull << 32)) {
         const uint32_t r = t->krec_len;
         delete t;
@@ -1482,6 +1528,8 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->occ);
     (void)hipFree(t->n_groups);
     (void)hipFree(t->dbg_cnt);
+    (void)hipFree(t->p_recs);
+    (void)hipFree(t->p_cnt);
     for (auto *p : t->text) (void)hipFree(p);
     delete t;
     return IGX_OK;
@@ -1548,16 +1596,137 @@ static void launch_direct(igx_ctx *ctx, GbArgs &a) {
     else launch_direct_as<L, AMAX>(ctx, a);
 }
 
+static int grow(igx_ctx *ctx, void **p, size_t *have, size_t need) {
+    if (*have >= need) return IGX_OK;
+    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));   // the old buffer may still be in use
+    (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    IGX_HIP(ctx, hipMalloc(p, need));
+    *have = need;
+    return IGX_OK;
+}
+
+// The partitioned form (k_groupby_part.h): passes A, S, B, I, C.
+template <class L, int NA>
+static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a) {
+    constexpr int KW = L::KW;
+    PartArgs p{};
+    // record layout: key words, then the loaded value / condition columns, then the index
+    uint32_t wp = KW;
+    for (uint32_t x = 0; x < t->naggs; ++x) {
+        if (a.vload[x]) {
+            p.vpos[x] = wp;
+            p.vw2[x] = a.vwidth[x] == 8;
+            wp += 1 + p.vw2[x];
+        }
+        if (a.cload[x]) {
+            p.cpos[x] = wp;
+            p.cw2[x] = a.cwidth[x] == 8;
+            wp += 1 + p.cw2[x];
+        }
+    }
+    p.iw = a.fidx ? 2 : 1;
+    p.ipos = wp;
+    wp += p.iw;
+    p.rq = (4 * wp + 15) / 16;
+    // tiles of A and B: as many records (a power of two in [PTS, 4096]) as fit the staging LDS
+    // with their bucket and permutation entries, so that several blocks share a CU
+    const size_t per_rec = 16 * (size_t)p.rq + 4;
+    uint32_t tr = 4096;
+    while (tr > PTS && (size_t)tr * per_rec > PART_TILE_LDS) tr >>= 1;
+    if ((size_t)tr * per_rec > 136 * 1024)
+        return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: rows of %u B are too wide for the partitioned form",
+                        16 * p.rq);
+    p.tr1 = p.tr2 = tr;
+    // final buckets small enough that the expected groups of one (from the table's capacity)
+    // fill at most half of the LDS table; each owns whole probe regions
+    const size_t entry = 8 + 8 * (size_t)t->naggs + 8 + 4 * (size_t)KW;
+    const uint32_t lb_min = t->sbits > 15 ? t->sbits - 15 : 0;   // <= 32K slots per bucket
+    const uint32_t lb_max = std::min<uint32_t>(t->sbits - t->rbits, 28);
+    auto entries = [&](uint32_t lb) {
+        const size_t occw = (size_t)1 << (t->sbits - lb - 5);
+        return (PART_AGG_LDS - 8 * occw - 4 * (2 * PSEG + 1) - 4 * (PT / 64) - 64) / entry;
+    };
+    uint32_t lb = lb_min;
+    while (lb < lb_max && (t->cap >> lb) * 2 > entries(lb)) ++lb;
+    p.f1 = (lb + 1) / 2;
+    p.f2 = lb / 2;
+    p.sb_log = t->sbits - lb;
+    p.occw = 1u << (p.sb_log - 5);
+    p.E = (uint32_t)entries(lb);
+    if (const char *d = std::getenv("IGX_GBP_ENTRIES"))   // tests: a small LDS table overflows
+        p.E = std::max<uint32_t>(8, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0)));
+    p.maxp = std::min<uint32_t>(p.E, 512);
+    if (const char *d = std::getenv("IGX_GBP_DEBUG")) p.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
+    const uint32_t F1 = 1u << p.f1, F2 = 1u << p.f2, nb = 1u << lb;
+    p.ch = (uint32_t)std::max<uint64_t>(16384, 4 * (a.n / nb + 1));
+    p.tiles1 = (uint32_t)((a.n + p.tr1 - 1) / p.tr1);
+    p.tiles2max = (uint32_t)((a.n + p.tr2 - 1) / p.tr2) + F1;
+    // scratch: h1 | p1 | base1 | t2base | h2 | items (u32 words), records of A and B
+    const uint64_t w_h1 = (uint64_t)p.tiles1 * (F1 + 1), w_p1 = (uint64_t)F1 * (p.tiles1 + 1);
+    const uint64_t w_h2 = (uint64_t)p.tiles2max * (F2 + 1);
+    p.imax = (uint32_t)std::min<uint64_t>(0xFFFFFFFFu, 2ull * nb + a.n / p.ch + 2);
+    const uint64_t words = w_h1 + w_p1 + 2 * (F1 + 1) + w_h2 + nb + 1 + 3ull * p.tiles2max + p.imax;
+    const size_t rec_bytes = (size_t)16 * p.rq;
+    int rc = grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
+    if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes,
+                       rec_bytes * ((uint64_t)p.tiles1 * p.tr1 + a.n));
+    if (rc) return rc;
+    p.h1 = t->p_cnt;
+    p.p1 = p.h1 + w_h1;
+    p.base1 = p.p1 + w_p1;
+    p.t2base = p.base1 + F1 + 1;
+    p.h2 = p.t2base + F1 + 1;
+    p.items = p.h2 + w_h2;
+    p.bmap = p.items + nb + 1;
+    p.imap = p.bmap + 3ull * p.tiles2max;
+    p.recs1 = t->p_recs;
+    p.recs2 = t->p_recs + (uint64_t)p.tiles1 * p.tr1 * p.rq * 4;
+    const size_t lds_a = (size_t)p.tr1 * (rec_bytes + 4) + 4 * (F1 + 1) + 4 * 17;
+    const size_t lds_b = (size_t)p.tr2 * (rec_bytes + 4) + 4 * (F2 + 1) + 4 * 17 + 4 * (2 * PSEGB + 1) + p.tr2 / 16;
+    const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 4 * (2 * PSEG + 1) + 4 * (PT / 64) + 64;
+    static size_t lds_set[3] = {0, 0, 0};   // dynamic LDS granted to each kernel so far
+    const void *kern[3] = {reinterpret_cast<const void *>(k_gbp_a<L, NA>),
+                           reinterpret_cast<const void *>(k_gbp_b<KW, NA>),
+                           reinterpret_cast<const void *>(k_gbp_c<KW, NA>)};
+    const size_t need[3] = {lds_a, lds_b, lds_c};
+    for (int i = 0; i < 3; ++i) {
+        if (need[i] > lds_set[i]) {
+            IGX_HIP(ctx, hipFuncSetAttribute(kern[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[i]));
+            lds_set[i] = need[i];
+        }
+    }
+    hipLaunchKernelGGL((k_gbp_a<L, NA>), dim3(p.tiles1), dim3(PTS), lds_a, ctx->stream, a, p);
+    hipLaunchKernelGGL(k_gbp_colscan, dim3(F1), dim3(1024), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_base, dim3(1), dim3(1024), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_bmap, dim3((p.tiles2max + 255) / 256), dim3(256), 0, ctx->stream, p);
+    hipLaunchKernelGGL((k_gbp_b<KW, NA>), dim3(p.tiles2max), dim3(PTS), lds_b, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_icount, dim3(F1), dim3(256), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_iscan, dim3(1), dim3(1024), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_imap, dim3(256), dim3(256), 0, ctx->stream, p);
+    hipLaunchKernelGGL((k_gbp_c<KW, NA>), dim3((unsigned)ctx->num_cus), dim3(PT), lds_c, ctx->stream, a, p);
+    return IGX_OK;
+}
+
+template <class L>
+static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
+    if (a.naggs <= 2) return launch_part_as<L, 2>(t, ctx, a);
+    return launch_part_as<L, AMAX>(t, ctx, a);
+}
+
 // one update over layout L in the interval's form
 template <class L>
-static void launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+    if (t->interval_part) return launch_part<L>(t, ctx, a);
     if (t->interval_direct) launch_direct<L>(ctx, a);
     else launch_gb<L>(ctx, a, blocks);
+    return IGX_OK;
 }
 
 extern "C" int igx_groupby_set_mode(igx_table *t, uint32_t mode) {
     if (!t) return IGX_EINVAL;
-    if (mode > IGX_GB_DIRECT) return igx_fail(t->ctx, IGX_EINVAL, "groupby_set_mode: mode %u", mode);
+    if (mode > IGX_GB_PART) return igx_fail(t->ctx, IGX_EINVAL, "groupby_set_mode: mode %u", mode);
     t->mode = mode;
     t->direct_left = 0;
     return IGX_OK;
@@ -1721,8 +1890,9 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.err = t->err;
     a.occ = t->occ;
     a.ep = t->ep;
-    a.mask = t->nslots - 1;
-    a.max_probe = (uint32_t)std::min<uint64_t>(t->nslots, 1u << 20);
+    a.sshift = 64 - t->sbits;
+    a.rmask = (1ull << t->rbits) - 1;
+    a.max_probe = 1u << t->rbits;
     if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
     a.nl = NL_DEFAULT;
     if (const char *d = std::getenv("IGX_GB_LOADERS")) {   // tuning knob
@@ -1743,32 +1913,35 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     // is only meaningful for a whole interval of the cached form)
     if (t->rows_fed == nrows) {
         t->interval_direct = t->mode == IGX_GB_DIRECT || (t->mode == IGX_GB_AUTO && t->direct_left > 0);
+        t->interval_part = t->mode == IGX_GB_PART;
         if (t->mode == IGX_GB_AUTO && t->direct_left > 0) --t->direct_left;
     }
-    if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = false;   // diagnostics run the cached form
+    if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = t->interval_part = false;   // diagnostics: cached form
+    int rc = IGX_OK;
     if (t->generic) {
         switch (t->kw_rec) {
-        case 2: launch_form<GenericLayout<2>>(t, ctx, a, blocks); break;
-        case 4: launch_form<GenericLayout<4>>(t, ctx, a, blocks); break;
-        case 6: launch_form<GenericLayout<6>>(t, ctx, a, blocks); break;
-        case 8: launch_form<GenericLayout<8>>(t, ctx, a, blocks); break;
-        case 12: launch_form<GenericLayout<12>>(t, ctx, a, blocks); break;
-        case 18: launch_form<GenericLayout<18>>(t, ctx, a, blocks); break;
-        case 24: launch_form<GenericLayout<24>>(t, ctx, a, blocks); break;
-        case 32: launch_form<GenericLayout<32>>(t, ctx, a, blocks); break;
+        case 2: rc = launch_form<GenericLayout<2>>(t, ctx, a, blocks); break;
+        case 4: rc = launch_form<GenericLayout<4>>(t, ctx, a, blocks); break;
+        case 6: rc = launch_form<GenericLayout<6>>(t, ctx, a, blocks); break;
+        case 8: rc = launch_form<GenericLayout<8>>(t, ctx, a, blocks); break;
+        case 12: rc = launch_form<GenericLayout<12>>(t, ctx, a, blocks); break;
+        case 18: rc = launch_form<GenericLayout<18>>(t, ctx, a, blocks); break;
+        case 24: rc = launch_form<GenericLayout<24>>(t, ctx, a, blocks); break;
+        case 32: rc = launch_form<GenericLayout<32>>(t, ctx, a, blocks); break;
         default: return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: no kernel for %u key words", t->kw_rec);
         }
-    } else if (layout_is<TcpKey>(kw, t->nkeys)) launch_form<TcpKey>(t, ctx, a, blocks);
-    else if (layout_is<FileKey>(kw, t->nkeys)) launch_form<FileKey>(t, ctx, a, blocks);
+    } else if (layout_is<TcpKey>(kw, t->nkeys)) rc = launch_form<TcpKey>(t, ctx, a, blocks);
+    else if (layout_is<FileKey>(kw, t->nkeys)) rc = launch_form<FileKey>(t, ctx, a, blocks);
     else if (layout_is<NetPolicyKey>(kw, t->nkeys))
-        launch_form<NetPolicyKey>(t, ctx, a, blocks);
-    else if (layout_is<BioKey>(kw, t->nkeys)) launch_form<BioKey>(t, ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 1) launch_form<StaticLayout<1>>(t, ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 2) launch_form<StaticLayout<2>>(t, ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 4) launch_form<StaticLayout<4>>(t, ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 8) launch_form<StaticLayout<8>>(t, ctx, a, blocks);
-    else if (t->nkeys == 1 && kw[0] == 16) launch_form<StaticLayout<16>>(t, ctx, a, blocks);
+        rc = launch_form<NetPolicyKey>(t, ctx, a, blocks);
+    else if (layout_is<BioKey>(kw, t->nkeys)) rc = launch_form<BioKey>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 1) rc = launch_form<StaticLayout<1>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 2) rc = launch_form<StaticLayout<2>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 4) rc = launch_form<StaticLayout<4>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 8) rc = launch_form<StaticLayout<8>>(t, ctx, a, blocks);
+    else if (t->nkeys == 1 && kw[0] == 16) rc = launch_form<StaticLayout<16>>(t, ctx, a, blocks);
     else return igx_fail(ctx, IGX_EINVAL, "groupby_update: internal layout mismatch");
+    if (rc) return rc;
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }
@@ -1800,7 +1973,7 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When
     // nearly every row missed, the cache is pure overhead: AUTO runs the next DIRECT_RUN
     // intervals in the direct form, then one cached interval to measure again.
-    if (t->rows_fed >= 1000000 && !t->interval_direct) {
+    if (t->rows_fed >= 1000000 && !t->interval_direct && !t->interval_part) {
         t->prefer_sm = misses * 10 > t->rows_fed * 7;
         if (t->mode == IGX_GB_AUTO && misses * 100 > t->rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }

@@ -218,7 +218,7 @@ class Table:
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
 
     def set_mode(self, mode):
-        """igx_groupby_set_mode: _abi.GB_AUTO (default), GB_CACHED or GB_DIRECT."""
+        """igx_groupby_set_mode: _abi.GB_AUTO (default), GB_CACHED, GB_DIRECT or GB_PART."""
         self.ctx.check(self.ctx.L.igx_groupby_set_mode(self.h, mode))
 
     def finalize(self):

@@ -416,3 +416,78 @@ def test_direct_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layou
         tab.update(cols, list(range(len(names))), n, 9, valid=dv)
         _check(E, H, tab, widths, *o)
     tab.destroy()
+
+
+@pytest.mark.parametrize("variant", ["plain", "skewed", "lds_overflow", "index_column"])
+@pytest.mark.parametrize("layout", ["tcp", "file", "np_distinct", "generic"])
+def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layout, variant):
+    """IGX_GB_PART (k_groupby_part.h: count, scan, scatter into hash buckets, LDS aggregation
+    per bucket, plain writes into the bucket's own probe regions) gives the oracle's table --
+    keys, every aggregate (incl. a u32 wrap), first index -- over three chunked updates with a
+    running base index and a nil mask.  'skewed': one key holds a large share of the rows, so
+    its bucket is split into several work items that merge with CAS claims and atomics;
+    'lds_overflow': an 8-entry LDS table sends most rows down the HBM path; 'index_column':
+    global indices from a u64 column (the owner-side merge of igx_dist_exchange_groups)."""
+    A = igx._abi
+    n = 450_000
+    rng = np.random.default_rng(11)
+    s = 1.3 if variant == "skewed" else 0.5
+    if layout == "tcp":
+        G = 40_000
+        ev_h = oracle.gen_tcp(0xC2, 3, G, oracle.zipf_cdf(G, s), 0, n)
+        names, widths = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family"), \
+            [16, 16, 8, 4, 16, 2, 2, 2]
+        extra = ("size", "dir")
+        aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 4, 1)]
+        oaggs = [{"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 0},
+                 {"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 1, "out_width": 4}]
+    elif layout == "file":
+        G = 100_000
+        ev_h = oracle.gen_file(0xC5, 0, G, oracle.zipf_cdf(G, s), 0, n)
+        names, widths, extra = ("inode", "dev", "pid", "tid"), [8, 4, 4, 4], ("op", "count")
+        aggs = [A.Agg(A.AGG_COUNT, 0, 4, 8, 0), A.Agg(A.AGG_SUM, 5, 4, 8, 0),
+                A.Agg(A.AGG_COUNT, 0, 4, 8, 1), A.Agg(A.AGG_SUM, 5, 4, 4, 1)]
+        oaggs = [{"kind": "count", "cond": ev_h["op"], "cond_val": 0},
+                 {"kind": "sum", "val": ev_h["count"], "cond": ev_h["op"], "cond_val": 0},
+                 {"kind": "count", "cond": ev_h["op"], "cond_val": 1},
+                 {"kind": "sum", "val": ev_h["count"], "cond": ev_h["op"], "cond_val": 1, "out_width": 4}]
+    elif layout == "np_distinct":
+        ev_h = oracle.gen_np(0xC4, 5_000 if variant != "skewed" else 40, 50_000, 0, n)
+        names, widths, extra, aggs, oaggs = ("src", "pkt", "peer", "port"), [4, 1, 4, 2], (), [], []
+    else:
+        G = 30_000
+        ev_h = oracle.gen_tcp(0xC2, 5, G, oracle.zipf_cdf(G, s + 0.3), 0, n)
+        names, widths, extra = ("pid", "lport", "dir"), [4, 2, 1], ("size",)
+        aggs = [A.Agg(A.AGG_SUM, 3, A.NO_COL, 8, 0)]
+        oaggs = [{"kind": "sum", "val": ev_h["size"]}]
+    if variant == "lds_overflow":
+        monkeypatch.setenv("IGX_GBP_ENTRIES", "8")
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    cols = [ev[k] for k in names + extra]
+    idx_h = None
+    if variant == "index_column":   # a permutation of global indices, not in row order
+        idx_h = (rng.permutation(n).astype(np.uint64) * np.uint64(3) + np.uint64(1000))
+        cols = cols + [H.to_device(idx_h)]
+    o = oracle.groupby(oracle.pack_cols(ev_h, names), oaggs, valid=valid, base_idx=9)
+    if idx_h is not None:   # first = the smallest index column value of the group's rows
+        packed = oracle.pack_cols(ev_h, names)
+        okeys = [bytes(k) for k in o[0]]
+        pos = {k: i for i, k in enumerate(okeys)}
+        first = np.full(len(okeys), np.iinfo(np.uint64).max, dtype=np.uint64)
+        for r in np.nonzero(valid)[0]:
+            i = pos[bytes(packed[r])]
+            first[i] = min(first[i], idx_h[r])
+        o = (o[0], o[1], first)
+    tab = E.Table(widths, aggs, n)
+    tab.set_mode(A.GB_PART)
+    dv = H.to_device(valid)
+    cuts = [0, n // 3, 2 * n // 3, n]
+    icol = len(names) + len(extra) if idx_h is not None else None
+    for a, b in zip(cuts, cuts[1:]):
+        tab.update([c[a:b] for c in cols], list(range(len(names))), b - a, 9 + a, valid=dv[a:b], idx_col=icol)
+    _check(E, H, tab, widths, *o)
+    tab.reset()                                            # a second interval, one update
+    tab.update(cols, list(range(len(names))), n, 9, valid=dv, idx_col=icol)
+    _check(E, H, tab, widths, *o)
+    tab.destroy()
