@@ -4,16 +4,22 @@
 //
 // Semantics follow Go's regexp on a string: the text is a sequence of runes decoded with
 // utf8.DecodeRune (an invalid byte is one U+FFFD rune), MatchString is an unanchored search,
-// `.` is any rune but '\n' (any rune with (?s)), `^`/`$` are the text's ends ((?m) is not
-// supported), \d \s \w and the POSIX-free classes are ASCII as in RE2, and (?i) folds ASCII
-// letters with their simple-fold orbits (k ↔ K ↔ U+212A, s ↔ S ↔ U+017F).  Unsupported
-// syntax (\b, \pN, (?m), non-ASCII literals under (?i), backreferences do not exist in RE2)
-// makes igx_filter return IGX_ENOTSUP; syntax errors surface at igx_filter_parse.
+// `.` is any rune but '\n' (any rune with (?s)), `^`/`$` are the text's ends, or line ends
+// under (?m); \A \z \b \B are RE2's empty-width assertions (\b on ASCII word runes), \d \s
+// \w and the [[:name:]] classes are ASCII as in RE2, \pN / \p{Name} are Unicode general
+// categories (igx_unicode.h, Unicode 13.0.0 like Go 1.19), and (?i) folds every rune with its
+// simple-fold orbit (k ↔ K ↔ U+212A, s ↔ S ↔ U+017F, ...) -- classes too, as Go's parser
+// folds them.  Script names (\p{Greek}) are not compiled: IGX_ENOTSUP.  Syntax errors
+// surface at igx_filter_parse.
 //
-// Pipeline: recursive-descent parse -> Thompson NFA over rune sets -> alphabet split into
-// the elementary rune intervals the sets use -> subset construction with the search start
-// re-added at every position; per DFA state, "matched" (a match ended here: the search can
-// stop) and "matches at end" (a match that needs `$`).
+// Pipeline: recursive-descent parse -> Thompson NFA over rune sets and empty-width
+// assertions -> alphabet split into the elementary rune intervals the sets use (word runes
+// and '\n' always get intervals of their own) -> subset construction.  A DFA state is a set
+// of NFA states plus the context of the previous rune (start of text / '\n' / word rune /
+// other): on the next rune the assertions that hold between the two are known, the set is
+// closed over them and, if a match is complete there, the transition goes to the absorbing
+// accept state; otherwise the search start is re-added.  Per state, bit1 of the flags says
+// whether a match completes at the end of the text (`$`, `\z`, `\b` before the end).
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -23,6 +29,7 @@
 
 #include "igx_internal.h"
 #include "igx_regex.h"
+#include "igx_unicode.h"
 
 namespace {
 
@@ -51,26 +58,89 @@ Ranges negate(const Ranges &r) {
     return o;
 }
 
-// simple-fold orbit of an ASCII letter (unicode.SimpleFold)
-void add_fold(Ranges &r, uint32_t c) {
-    r.push_back({c, c});
-    if (c >= 'a' && c <= 'z') r.push_back({c - 32, c - 32});
-    if (c >= 'A' && c <= 'Z') r.push_back({c + 32, c + 32});
-    if (c == 'k' || c == 'K') r.push_back({0x212A, 0x212A});
-    if (c == 's' || c == 'S') r.push_back({0x17F, 0x17F});
+// simple-fold orbits (unicode.SimpleFold): rune -> orbit members, from igx_unicode.h
+const std::map<uint32_t, std::vector<uint32_t>> &fold_orbits() {
+    static const std::map<uint32_t, std::vector<uint32_t>> m = [] {
+        std::map<uint32_t, std::vector<uint32_t>> by_key, by_rune;
+        for (const auto &f : igx_unicode::kFolds) by_key[f.key].push_back(f.r);
+        for (const auto &f : igx_unicode::kFolds) by_rune[f.r] = by_key[f.key];
+        return by_rune;
+    }();
+    return m;
 }
 
-enum NType : uint8_t { N_SET, N_SPLIT, N_EPS, N_BEGIN, N_END, N_MATCH };
+void add_fold(Ranges &r, uint32_t c) {
+    r.push_back({c, c});
+    const auto &m = fold_orbits();
+    auto it = m.find(c);
+    if (it != m.end())
+        for (uint32_t o : it->second) r.push_back({o, o});
+}
+
+// a class under (?i): every rune's orbit (appendFoldedClass in Go's regexp/syntax)
+Ranges fold_ranges(const Ranges &in) {
+    Ranges r = in;
+    const auto &m = fold_orbits();
+    for (const auto &p : in)
+        for (auto it = m.lower_bound(p.first); it != m.end() && it->first <= p.second; ++it)
+            for (uint32_t o : it->second) r.push_back({o, o});
+    return normalize(r);
+}
+
+// Go's regexp/syntax EmptyOp bits
+enum : uint8_t { E_BEGIN_LINE = 1, E_END_LINE = 2, E_BEGIN_TEXT = 4, E_END_TEXT = 8, E_WORD = 16, E_NOWORD = 32 };
+
+enum NType : uint8_t { N_SET, N_SPLIT, N_EPS, N_ASSERT, N_MATCH };
 struct NState {
     NType t;
-    int set = -1;        // rune-set id (N_SET)
+    int set = -1;        // rune-set id (N_SET); the EmptyOp (N_ASSERT)
     int out = -1, out2 = -1;
 };
+
+bool word_rune(uint32_t c) {
+    return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+}
+
+// \p{Name}: a general category (two letters, or one letter for the major class), or Any
+bool unicode_class(const std::string &name, Ranges *out) {
+    Ranges r;
+    if (name == "Any") {
+        *out = {{0, MAXRUNE}};
+        return true;
+    }
+    bool any = false;
+    for (int k = 0; k < igx_unicode::kNumCats; ++k) {
+        const char *c = igx_unicode::kCats[k];
+        if (name == c || (name.size() == 1 && name[0] == c[0])) {
+            any = true;
+            for (const auto &x : igx_unicode::kCatRanges)
+                if (x.cat == k) r.push_back({x.lo, x.hi});
+        }
+    }
+    if (!any) return false;
+    *out = normalize(r);
+    return true;
+}
+
+// [[:name:]] (RE2's ASCII POSIX classes)
+bool posix_class(const std::string &name, Ranges *out) {
+    static const std::map<std::string, Ranges> t = {
+        {"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}}, {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+        {"ascii", {{0, 0x7F}}}, {"blank", {{'\t', '\t'}, {' ', ' '}}}, {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+        {"digit", {{'0', '9'}}}, {"graph", {{'!', '~'}}}, {"lower", {{'a', 'z'}}}, {"print", {{' ', '~'}}},
+        {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}}, {"space", {{'\t', '\r'}, {' ', ' '}}},
+        {"upper", {{'A', 'Z'}}}, {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+        {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}}};
+    auto it = t.find(name);
+    if (it == t.end()) return false;
+    *out = normalize(it->second);
+    return true;
+}
 
 struct Compiler {
     std::string re;
     size_t i = 0;
-    bool icase = false, dotnl = false;
+    bool icase = false, dotnl = false, multiline = false;
     std::string err;       // syntax error (parse) -> EINVAL
     bool unsup = false;    // valid RE2 we do not compile -> ENOTSUP
     std::vector<NState> st;
@@ -95,6 +165,7 @@ struct Compiler {
         return single(N_SET, (int)sets.size() - 1);
     }
     F empty() { return single(N_EPS); }
+    F assertion(uint8_t op) { return single(N_ASSERT, op); }
     F cat(F a, F b) {
         patch(a.outs, b.start);
         return F{a.start, b.outs};
@@ -145,10 +216,44 @@ struct Compiler {
 
     Ranges literal_set(uint32_t c) {
         Ranges r;
-        if (icase && ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'))) add_fold(r, c);
-        else if (icase && c >= 0x80) { unsup = true; r.push_back({c, c}); }
+        if (icase) add_fold(r, c);
         else r.push_back({c, c});
         return r;
+    }
+
+    // a class escape or [:name:] group under the current flags (Go's appendGroup: folded
+    // first, then negated)
+    Ranges group(const Ranges &cls, bool neg) {
+        const Ranges c = icase ? fold_ranges(cls) : normalize(cls);
+        return neg ? negate(c) : c;
+    }
+
+    // \pN, \p{Name}, \p{^Name}, \PN (after the 'p' / 'P'); false with err / unsup set
+    bool unicode_escape(bool neg, Ranges *out) {
+        if (eof()) { err = "invalid character class range"; return false; }
+        std::string name;
+        if (peek() == '{') {
+            const size_t e = re.find('}', i);
+            if (e == std::string::npos) { err = "invalid character class range"; return false; }
+            name = re.substr(i + 1, e - i - 1);
+            i = e + 1;
+        } else {
+            uint32_t c;
+            if (!pat_rune(&c)) return false;
+            name = std::string(1, (char)c);
+        }
+        if (!name.empty() && name[0] == '^') {
+            neg = !neg;
+            name = name.substr(1);
+        }
+        Ranges r;
+        if (!unicode_class(name, &r)) {
+            // a script name (\p{Greek}) or an unknown one: not compiled here
+            unsup = true;
+            return false;
+        }
+        *out = group(r, neg);
+        return true;
     }
 
     // escapes usable inside and outside classes; returns false with err/unsup set
@@ -156,13 +261,17 @@ struct Compiler {
         if (eof()) { err = "trailing backslash at end of expression"; return false; }
         const char c = re[i++];
         *is_class = true;
+        const Ranges digit = {{'0', '9'}}, space = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}},
+                     word = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
         switch (c) {
-        case 'd': *out = {{'0', '9'}}; return true;
-        case 'D': *out = negate({{'0', '9'}}); return true;
-        case 's': *out = normalize({{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}}); return true;
-        case 'S': *out = negate(normalize({{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}})); return true;
-        case 'w': *out = normalize({{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}); return true;
-        case 'W': *out = negate(normalize({{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}})); return true;
+        case 'd': *out = group(digit, false); return true;
+        case 'D': *out = group(digit, true); return true;
+        case 's': *out = group(space, false); return true;
+        case 'S': *out = group(space, true); return true;
+        case 'w': *out = group(word, false); return true;
+        case 'W': *out = group(word, true); return true;
+        case 'p': return unicode_escape(false, out);
+        case 'P': return unicode_escape(true, out);
         default: break;
         }
         *is_class = false;
@@ -174,6 +283,16 @@ struct Compiler {
         case 'f': v = '\f'; break;
         case 'v': v = '\v'; break;
         case 'a': v = 7; break;
+        case '1': case '2': case '3': case '4': case '5': case '6': case '7':
+            // a lone non-zero digit would be a backreference (not RE2); with more octal
+            // digits it is an octal escape
+            if (eof() || peek() < '0' || peek() > '7') { err = "invalid escape sequence"; return false; }
+            [[fallthrough]];
+        case '0': {
+            v = (uint32_t)(c - '0');
+            for (int k = 0; k < 2 && !eof() && peek() >= '0' && peek() <= '7'; ++k) v = v * 8 + (uint32_t)(re[i++] - '0');
+            break;
+        }
         case 'x': {
             auto hex = [](char h) { return h >= '0' && h <= '9' ? h - '0' : h >= 'a' && h <= 'f' ? h - 'a' + 10 :
                                            h >= 'A' && h <= 'F' ? h - 'A' + 10 : -1; };
@@ -198,9 +317,7 @@ struct Compiler {
         }
         default:
             if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) {
-                // \b \B \A \z \pN \Q ... : valid RE2 we do not compile, or invalid
-                if (std::strchr("bBAzpPQECz", c)) unsup = true;
-                else err = "invalid escape sequence";
+                err = "invalid escape sequence";   // \b \B \A \z \Q are handled before this
                 return false;
             }
             v = (unsigned char)c;   // escaped punctuation
@@ -216,7 +333,20 @@ struct Compiler {
         bool first = true;
         while (!eof() && (peek() != ']' || first)) {
             first = false;
-            if (peek() == '[' && i + 1 < re.size() && re[i + 1] == ':') { unsup = true; return false; }   // [:alpha:]
+            if (peek() == '[' && i + 1 < re.size() && re[i + 1] == ':') {   // [:alpha:], [:^alpha:]
+                const size_t e = re.find(":]", i + 2);
+                if (e != std::string::npos) {
+                    std::string name = re.substr(i + 2, e - i - 2);
+                    bool pneg = false;
+                    if (!name.empty() && name[0] == '^') { pneg = true; name = name.substr(1); }
+                    Ranges g;
+                    if (!posix_class(name, &g)) { err = "invalid character class range"; return false; }
+                    const Ranges x = group(g, pneg);
+                    r.insert(r.end(), x.begin(), x.end());
+                    i = e + 2;
+                    continue;
+                }
+            }
             uint32_t lo;
             if (peek() == '\\') {
                 ++i;
@@ -244,8 +374,8 @@ struct Compiler {
                 if (hi < lo) { err = "invalid character class range"; return false; }
             }
             if (icase) {
-                for (uint32_t c = lo; c <= hi && c < 0x80; ++c) add_fold(r, c);
-                if (hi >= 0x80) { unsup = true; r.push_back({std::max(lo, 0x80u), hi}); }
+                const Ranges x = fold_ranges({{lo, hi}});
+                r.insert(r.end(), x.begin(), x.end());
             } else {
                 r.push_back({lo, hi});
             }
@@ -261,7 +391,7 @@ struct Compiler {
         const char c = peek();
         if (c == '(') {
             ++i;
-            bool save_i = icase, save_s = dotnl;
+            bool save_i = icase, save_s = dotnl, save_m = multiline;
             if (!eof() && peek() == '?') {
                 ++i;
                 if (!eof() && (peek() == 'P' || peek() == '<')) {   // named group
@@ -277,7 +407,7 @@ struct Compiler {
                         else if (fc == 'i') icase = on;
                         else if (fc == 's') dotnl = on;
                         else if (fc == 'U') { /* ungreedy: no effect on match/no match */ }
-                        else if (fc == 'm') { unsup = true; return false; }
+                        else if (fc == 'm') multiline = on;
                         else { err = "invalid or unsupported Perl syntax"; return false; }
                     }
                     if (eof()) { err = "missing closing )"; return false; }
@@ -296,6 +426,7 @@ struct Compiler {
             ++i;
             icase = save_i;
             dotnl = save_s;
+            multiline = save_m;
             *f = inner;
             return true;
         }
@@ -311,8 +442,29 @@ struct Compiler {
             *f = set_frag(dotnl ? Ranges{{0, MAXRUNE}} : negate({{'\n', '\n'}}));
             return true;
         }
-        if (c == '^') { ++i; *f = single(N_BEGIN); return true; }
-        if (c == '$') { ++i; *f = single(N_END); return true; }
+        if (c == '^') { ++i; *f = assertion(multiline ? E_BEGIN_LINE : E_BEGIN_TEXT); return true; }
+        if (c == '$') { ++i; *f = assertion(multiline ? E_END_LINE : E_END_TEXT); return true; }
+        if (c == '\\' && i + 1 < re.size()) {
+            const char e = re[i + 1];
+            if (e == 'A') { i += 2; *f = assertion(E_BEGIN_TEXT); return true; }
+            if (e == 'z') { i += 2; *f = assertion(E_END_TEXT); return true; }
+            if (e == 'b') { i += 2; *f = assertion(E_WORD); return true; }
+            if (e == 'B') { i += 2; *f = assertion(E_NOWORD); return true; }
+            if (e == 'Q') {   // literal text up to \E (or the end of the pattern)
+                i += 2;
+                const size_t q = re.find("\\E", i);
+                const size_t end = q == std::string::npos ? re.size() : q;
+                F acc = empty();
+                while (i < end) {
+                    uint32_t rn;
+                    if (!pat_rune(&rn)) return false;
+                    acc = cat(acc, set_frag(literal_set(rn)));
+                }
+                if (q != std::string::npos) i = q + 2;
+                *f = acc;
+                return true;
+            }
+        }
         if (c == '\\') {
             ++i;
             Ranges r;
@@ -437,8 +589,9 @@ struct Compiler {
     }
 };
 
-// epsilon closure; BEGIN edges only when begin, END edges only when end
-void closure(const std::vector<NState> &st, std::vector<int> &set, bool begin, bool end) {
+// epsilon closure over splits and the assertions that hold (`ops`); keeps rune sets and
+// the match state
+void closure(const std::vector<NState> &st, std::vector<int> &set, uint8_t ops) {
     std::vector<char> seen(st.size(), 0);
     std::vector<int> stack(set.begin(), set.end());
     std::vector<int> out;
@@ -451,16 +604,27 @@ void closure(const std::vector<NState> &st, std::vector<int> &set, bool begin, b
         switch (x.t) {
         case N_SPLIT: stack.push_back(x.out); stack.push_back(x.out2); break;
         case N_EPS: stack.push_back(x.out); break;
-        case N_BEGIN: if (begin) stack.push_back(x.out); break;   // else: can never fire again
-        case N_END:
-            if (end) stack.push_back(x.out);
-            else out.push_back(s);   // pending: expanded at the end of the text
-            break;
+        case N_ASSERT: if (((uint8_t)x.set & ~ops) == 0) stack.push_back(x.out); break;
         default: out.push_back(s); break;   // N_SET, N_MATCH
         }
     }
     std::sort(out.begin(), out.end());
     set.swap(out);
+}
+
+// context of the previous rune: the start of the text, '\n', a word rune, anything else
+enum Ctx : uint8_t { C_BEGIN = 0, C_NL = 1, C_WORD = 2, C_OTHER = 3 };
+
+// the assertions that hold between a previous rune of context `c` and the next rune (or the
+// end of the text): emptyOpContext in Go's regexp/syntax
+uint8_t ops_between(uint8_t c, bool end, bool next_nl, bool next_word) {
+    uint8_t op = 0;
+    if (c == C_BEGIN) op |= E_BEGIN_TEXT | E_BEGIN_LINE;
+    if (c == C_NL) op |= E_BEGIN_LINE;
+    if (end) op |= E_END_TEXT | E_END_LINE;
+    if (next_nl) op |= E_END_LINE;
+    op |= ((c == C_WORD) != (!end && next_word)) ? E_WORD : E_NOWORD;
+    return op;
 }
 
 }  // namespace
@@ -479,8 +643,18 @@ int igx_regex_compile(const char *pattern, size_t len, RegexDfa *dfa, std::strin
     c.patch(f.outs, match);
     const int start = f.start;
     const auto &st = c.st;
-    // alphabet: elementary intervals of all sets
-    std::set<uint32_t> cuts = {0, MAXRUNE + 1};
+    // which parts of the previous rune's context any assertion reads
+    uint8_t used = 0;
+    for (const auto &x : st)
+        if (x.t == N_ASSERT) used |= (uint8_t)x.set;
+    const bool need_nl = used & (E_BEGIN_LINE | E_END_LINE), need_word = used & (E_WORD | E_NOWORD);
+    auto ctx_of = [&](bool nl, bool word) -> uint8_t {   // contexts that no assertion tells apart merge
+        if (nl && need_nl) return C_NL;
+        if (word && need_word) return C_WORD;
+        return C_OTHER;
+    };
+    // alphabet: elementary intervals of all sets; '\n' and the word runes always apart
+    std::set<uint32_t> cuts = {0, MAXRUNE + 1, '\n', '\n' + 1, '0', '9' + 1, 'A', 'Z' + 1, '_', '_' + 1, 'a', 'z' + 1};
     for (auto &r : c.sets)
         for (auto &p : r) { cuts.insert(p.first); cuts.insert(p.second + 1); }
     std::vector<uint32_t> bounds(cuts.begin(), cuts.end());   // class k = [bounds[k], bounds[k+1])
@@ -494,46 +668,54 @@ int igx_regex_compile(const char *pattern, size_t len, RegexDfa *dfa, std::strin
             const uint32_t b = (uint32_t)(std::lower_bound(bounds.begin(), bounds.end(), p.second + 1) - bounds.begin());
             for (uint32_t k = a; k < b; ++k) in[s][k] = 1;
         }
-    std::map<std::vector<int>, int> ids;
-    std::vector<std::vector<int>> sets;
-    auto intern = [&](std::vector<int> v) {
-        auto it = ids.find(v);
+    // DFA states: (NFA states before closure, previous-rune context); state 0 accepts
+    std::map<std::pair<std::vector<int>, uint8_t>, int> ids;
+    std::vector<std::pair<std::vector<int>, uint8_t>> states = {{{}, C_OTHER}};
+    auto intern = [&](std::vector<int> v, uint8_t cx) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        auto key = std::make_pair(std::move(v), cx);
+        auto it = ids.find(key);
         if (it != ids.end()) return it->second;
-        const int id = (int)sets.size();
-        ids.emplace(v, id);
-        sets.push_back(std::move(v));
+        const int id = (int)states.size();
+        ids.emplace(key, id);
+        states.push_back(std::move(key));
         return id;
     };
-    std::vector<int> s0 = {start};
-    closure(st, s0, true, false);
-    const int d0 = intern(s0);
+    const int d0 = intern({start}, C_BEGIN);
     std::vector<uint16_t> trans;
     std::vector<uint8_t> flags;
-    for (size_t d = 0; d < sets.size(); ++d) {
-        if (sets.size() > RegexDfa::MAXSTATES) { *why = "regular expression needs too many automaton states"; return IGX_ENOTSUP; }
-        const std::vector<int> cur = sets[d];
-        uint8_t fl = 0;
-        if (std::binary_search(cur.begin(), cur.end(), match)) fl |= 1;
-        std::vector<int> e = cur;
-        closure(st, e, false, true);   // the pending `$` edges, at the end of the text
-        if (std::binary_search(e.begin(), e.end(), match)) fl |= 2;
-        if (d == (size_t)d0) {         // the empty text: `^` and `$` both hold
-            std::vector<int> e0 = {start};
-            closure(st, e0, true, true);
-            if (std::binary_search(e0.begin(), e0.end(), match)) fl |= 4;
+    for (size_t d = 0; d < states.size(); ++d) {
+        if (states.size() > RegexDfa::MAXSTATES) { *why = "regular expression needs too many automaton states"; return IGX_ENOTSUP; }
+        if (d == 0) {   // accept: absorbing
+            flags.push_back(1 | 2 | 4);
+            for (uint32_t k = 0; k < ncls; ++k) trans.push_back(0);
+            continue;
         }
+        const std::vector<int> cur = states[d].first;
+        const uint8_t cx = states[d].second;
+        uint8_t fl = 0;
+        std::vector<int> e = cur;
+        closure(st, e, ops_between(cx, true, false, false));   // the text ends here
+        if (std::binary_search(e.begin(), e.end(), match)) fl |= 2;
+        if (d == (size_t)d0 && (fl & 2)) fl |= 4;               // the empty text matches
         flags.push_back(fl);
         for (uint32_t k = 0; k < ncls; ++k) {
+            const bool nl = bounds[k] == '\n', word = word_rune(bounds[k]);
+            std::vector<int> x = cur;
+            closure(st, x, ops_between(cx, false, nl, word));
+            if (std::binary_search(x.begin(), x.end(), match)) {   // a match is complete before this rune
+                trans.push_back(0);
+                continue;
+            }
             std::vector<int> nx;
-            for (int s : cur)
+            for (int s : x)
                 if (st[s].t == N_SET && in[st[s].set][k]) nx.push_back(st[s].out);
             nx.push_back(start);   // unanchored search: a match may start at every rune
-            closure(st, nx, false, false);
-            trans.push_back((uint16_t)intern(nx));
+            trans.push_back((uint16_t)intern(std::move(nx), ctx_of(nl, word)));
         }
     }
-    // note: d0 is the state before the first rune; BEGIN edges were taken there only
-    dfa->nstates = (uint32_t)sets.size();
+    dfa->nstates = (uint32_t)states.size();
     dfa->ncls = ncls;
     dfa->start = (uint32_t)d0;
     dfa->trans = std::move(trans);

@@ -7,11 +7,12 @@
 
 struct RegexDfa {
     static constexpr uint32_t MAXSTATES = 2048;
-    static constexpr uint32_t MAXCLS = 255;
+    static constexpr uint32_t MAXCLS = 4096;   // ASCII runes always fall in the first 128 classes
     uint32_t nstates = 0, ncls = 0, start = 0;
     std::vector<uint16_t> trans;      // nstates x ncls
-    std::vector<uint8_t> flags;       // bit0 matched here, bit1 matches at the end of the text,
-                                      // bit2 (start state) the empty text matches
+    std::vector<uint8_t> flags;       // bit0 a match is complete (the absorbing accept state),
+                                      // bit1 a match completes if the text ends here, bit2
+                                      // (start state) the empty text matches
     std::vector<uint32_t> bounds;     // class k = runes [bounds[k], bounds[k+1]) (last: to U+10FFFF)
     uint8_t ascii[128] = {};          // class of each ASCII rune
 };

@@ -25,7 +25,10 @@ def _strings(n, seed=4):
 
 
 @pytest.mark.parametrize("rule", ["~^k", "~(?i)demo", "!~(?i)demo", "~er$", "~[0-9]", "~^.{4}$",
-                                  "~caf.", "~\\d+:\\d", "~^$", "~x{16}", "~(?s)a.b"])
+                                  "~caf.", "~\\d+:\\d", "~^$", "~x{16}", "~(?s)a.b",
+                                  # RE2 assertions, (?m), Unicode classes and folding
+                                  "~\\bdemo\\b", "~\\Bsh", "~(?m)^b$", "~(?i)CAFÉ", "~\\p{Ll}{4}$",
+                                  "!~[[:upper:]]", "~\\pL\\PL"])
 def test_regex_filter_on_device(oracle, igx, rule):
     H = igx.columns
     n = 100_003

@@ -119,8 +119,77 @@ def test_regex_errors_and_unsupported(igx):
     assert compile_blob(igx, b"a(b")[0] == igx._abi.IGX_EINVAL
     assert compile_blob(igx, b"[a")[0] == igx._abi.IGX_EINVAL
     assert compile_blob(igx, b"*a")[0] == igx._abi.IGX_EINVAL
-    for p in (rb"\bfoo", rb"\pL", b"(?m)^a", "(?i)é".encode()):
-        assert compile_blob(igx, p)[0] == igx._abi.IGX_ENOTSUP, p
+    assert compile_blob(igx, rb"[\b]")[0] == igx._abi.IGX_EINVAL      # no \b inside a class in RE2
+    assert compile_blob(igx, rb"\1")[0] == igx._abi.IGX_EINVAL        # backreferences do not exist
+    assert compile_blob(igx, rb"[[:nope:]]")[0] == igx._abi.IGX_EINVAL
+    # script names need tables Python's unicodedata does not carry: not compiled
+    assert compile_blob(igx, rb"\p{Greek}")[0] == igx._abi.IGX_ENOTSUP
+
+
+# Assertions and (?m): Python's re with re.ASCII has RE2's ASCII \b / \w and the same (?m)
+# ^ / $ (line starts after '\n', line ends before '\n'); \z is Python's \Z.
+ASSERT_PATTERNS = [r"\bfoo\b", r"\Bo\B", r"\bo", r"o\b", r"(?m)^a", r"(?m)b$", r"(?m)^$", r"\Afoo",
+                   r"foo\z", r"(?m)^\w+$", r"x\b|\by", r"\b", r"\B", r"^\b$", r"(?m:^b)c", r"a\b\s",
+                   r"(?m)a$\n^b", r"\d\b", r"(?m)\Ab"]
+ASSERT_TEXTS = [b"", b"foo", b"a foo b", b"food", b"xfoo", b"foo_", b"o", b"ooo", b"a\nb", b"b\na", b"\n",
+                b"\n\n", b"ab\ncd", b"x y", b"xy", b"a b", b"12 3", b"a\n", b"\nb", b"foo\n", b"bc", b"b\nbc",
+                b" ", b"-", b"_x_"]
+
+
+@pytest.mark.parametrize("pattern", ASSERT_PATTERNS)
+def test_regex_assertions_match_search(igx, pattern):
+    rc, blob = compile_blob(igx, pattern.encode())
+    assert rc == 0, blob
+    pr = re.compile(pattern.replace(r"\z", r"\Z"), re.ASCII)
+    for t in ASSERT_TEXTS:
+        want = pr.search(t.decode()) is not None
+        if pattern == r"\B" and t == b"":
+            want = True   # RE2: no word boundary between two non-word sides; Python's \B never matches ""
+        assert run_blob(blob, t) == want, (pattern, t)
+
+
+# Unicode case folding under (?i): Python's re in str mode folds with Unicode simple case
+# folding too (same Unicode version, 13.0.0, as Go 1.19).
+FOLD_PATTERNS = ["(?i)é", "(?i)straße", "(?i)[à-ö]+", "(?i)σ", "(?i)ǆ", "(?i)[a-z]", "(?i)ω", "(?i)k",
+                 "(?i)i", "(?i)[^a-z]", "(?i)θ", "(?i)ꙋ"]
+FOLD_TEXTS = ["É", "é", "e", "STRASSE", "STRAẞE", "straße", "ÀÖ", "àö", "×", "Σ", "ς", "σ", "ǅ", "Ǆ", "K",
+              "Ω", "Ω", "ω", "I", "i", "ſ", "1", "", "ϑ", "ϴ", "Θ", "ᲈ", "Ꙋ"]
+
+
+@pytest.mark.parametrize("pattern", FOLD_PATTERNS)
+def test_regex_unicode_folding(igx, pattern):
+    rc, blob = compile_blob(igx, pattern.encode())
+    assert rc == 0, blob
+    pr = re.compile(pattern)
+    for t in FOLD_TEXTS:
+        assert run_blob(blob, t.encode()) == (pr.search(t) is not None), (pattern, t)
+
+
+def test_regex_dotted_i_known_answers(igx):
+    """U+0130 and U+0131 have no simple case folding (CaseFolding.txt has only T / F entries),
+    so Go's (?i)i matches neither -- Python's re, which lower-cases, differs here."""
+    ok = lambda p, t: run_blob(compile_blob(igx, p.encode())[1], t.encode())   # noqa: E731
+    assert not ok("(?i)i", "İ") and not ok("(?i)i", "ı") and not ok("(?i)[a-z]", "İ")
+    assert ok("(?i)ı", "ı") and not ok("(?i)ı", "I") and ok("(?i)İ", "İ") and not ok("(?i)İ", "i")
+
+
+def test_regex_classes_known_answers(igx):
+    r"""\p{..} general categories, POSIX classes, \Q..\E and octal escapes (Go regexp
+    semantics; parity unpinned by reference vectors -- Go is not in this image)."""
+    ok = lambda p, t: run_blob(compile_blob(igx, p.encode())[1], t.encode())   # noqa: E731
+    assert ok(r"^\pL+$", "héllo") and not ok(r"^\pL+$", "h3llo")
+    assert ok(r"^\p{Lu}", "Émile") and not ok(r"^\p{Lu}", "émile")
+    assert ok(r"^\p{^Lu}", "émile") and ok(r"^\PL", "3a") and not ok(r"^\PL", "a3")
+    assert ok(r"\p{Nd}", "٣") and not ok(r"\pN", "abc") and ok(r"\pN", "½")
+    assert ok(r"^\p{Any}$", "€") and ok(r"\p{Zs}", "a\u00a0b") and ok(r"^\p{Sc}$", "€")
+    assert ok(r"(?i)\p{Lu}", "é")                    # Go folds \p classes under (?i)
+    assert ok(r"^[[:alpha:]]+$", "abcXYZ") and not ok(r"^[[:alpha:]]+$", "abc1")
+    assert ok(r"^[[:^digit:]]+$", "abc") and not ok(r"[[:^digit:]]", "123")
+    assert ok(r"^[[:xdigit:][:space:]]+$", "dead beef") and not ok(r"[[:upper:]]", "abc")
+    assert ok(r"(?i)[[:upper:]]", "abc")              # folded, like Go
+    assert ok(r"(?i)\w", "\u212a") and not ok(r"\w", "\u212a")   # K folds to k, \w is ASCII
+    assert ok(r"\Qa.b*\E", "xa.b*y") and not ok(r"\Qa.b*\E", "aab")
+    assert ok(r"^\101\060$", "A0") and ok(r"^\x{20ac}$", "€")   # octal escapes; values end at NUL
 
 
 def test_filter_table_regex_rows_on_the_automaton(igx):
