@@ -37,9 +37,11 @@
 // its HBM updates go to the server wave through an LDS ring (see "HBM atomics through an
 // LDS ring").  Eight waves stream rows, seven resolve misses, the sixteenth issues the atomics.  The
 // cache is committed with HBM atomics at the end.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "k_common.h"
 
@@ -75,11 +77,14 @@ __host__ __device__ constexpr uint32_t vrec_bytes(uint32_t naggs) { return pow2_
 struct GbArgs {
     // static layouts: one base pointer per key column
     const uint8_t *kcol[16];
-    // generic layout: word w = (dword at kptr[w] + row*kwidth[w] + koff[w]) & kmask[w]
+    // generic layout: word w = (dword at kptr[w] + row*kwidth[w] + koff[w]) & kmask[w], or,
+    // for a column whose width is neither 1, 2 nor a multiple of 4, its kbytes[w] bytes
+    // loaded one by one (such a column is not dword aligned)
     const uint8_t *kptr[KWMAX];
     uint32_t kwidth[KWMAX];
     uint32_t koff[KWMAX];
     uint32_t kmask[KWMAX];
+    uint32_t kbytes[KWMAX];
     // aggregates: value = SUM column (vwidth bytes) or 1 (COUNT), if cond column == cval
     const uint8_t *vptr[AMAX];
     const uint8_t *cptr[AMAX];
@@ -234,7 +239,16 @@ struct GenericLayout {
     static constexpr bool is_static = false;
     __device__ __forceinline__ static void load(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
 #pragma unroll
-        for (int w = 0; w < KW; ++w) k[w] = ldw(a.kptr[w], row * a.kwidth[w] + a.koff[w]) & a.kmask[w];
+        for (int w = 0; w < KW; ++w) {
+            const uint64_t off = row * a.kwidth[w] + a.koff[w];
+            if (a.kbytes[w]) {   // an unaligned column: byte loads (uniform branch)
+                uint32_t v = 0;
+                for (uint32_t b = 0; b < a.kbytes[w]; ++b) v |= (uint32_t)a.kptr[w][off + b] << (8 * b);
+                k[w] = v;
+            } else {
+                k[w] = ldw(a.kptr[w], off) & a.kmask[w];
+            }
+        }
     }
 };
 
@@ -1342,6 +1356,13 @@ __global__ void k_gather_rows(const uint8_t *__restrict__ krec, uint32_t krec_le
     }
 }
 
+// rows kept by `in` (nullable: all) and every predicate of dp -> out (u8; in may be out)
+__global__ __launch_bounds__(256) void k_pred_mask(DevPreds dp, const uint8_t *in, uint64_t n, uint8_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        out[i] = (uint8_t)((!in || in[i]) && preds_match_all(dp, i));
+}
+
 #include "k_groupby_part.h"
 
 }  // namespace
@@ -1383,10 +1404,12 @@ struct igx_table {
     size_t p_recs_bytes = 0;
     uint32_t *p_cnt = nullptr;   // counts / offsets, then scan tile sums, then work items
     size_t p_cnt_bytes = 0;
+    uint8_t *p_mask = nullptr;   // row mask of the predicates that are not fused (grow-only)
+    size_t p_mask_bytes = 0;
     uint64_t host_groups = 0;
     unsigned long long *dbg_cnt = nullptr;
-    uint8_t *text[8] = {};       // IP text of the groups, per IGX_TSRC_IPTEXT sort key
-    uint64_t text_rows[8] = {};
+    uint8_t *text[32] = {};      // IP text of the groups, per IGX_TSRC_IPTEXT sort key
+    uint64_t text_rows[32] = {};
 };
 
 // compile-time key layouts: the reference's BPF key structs + single-column keys
@@ -1435,7 +1458,7 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     uint32_t words = 0;
     for (uint32_t i = 0; i < nkeys; ++i) {
         const uint32_t w = key_widths[i];
-        if (w == 0 || w == 3 || (w > 4 && w % 4)) return igx_fail(ctx, IGX_ENOTSUP, "groupby: key width %u", w);
+        if (w == 0) return igx_fail(ctx, IGX_EINVAL, "groupby: key width 0");
         words += (w + 3) / 4;
     }
     if (words > KWMAX) return igx_fail(ctx, IGX_ENOTSUP, "groupby: key wider than %d bytes", KWMAX * 4);
@@ -1530,6 +1553,7 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->dbg_cnt);
     (void)hipFree(t->p_recs);
     (void)hipFree(t->p_cnt);
+    (void)hipFree(t->p_mask);
     for (auto *p : t->text) (void)hipFree(p);
     delete t;
     return IGX_OK;
@@ -1758,7 +1782,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
             return igx_fail(ctx, IGX_EINVAL, "groupby_update: key column %u width %u != %u", k, c.width,
                             t->key_widths[k]);
         const uint8_t *p = static_cast<const uint8_t *>(c.ptr);
-        const uintptr_t need = c.width >= 16 ? 16 : (c.width >= 4 ? 4 : c.width);
+        const bool odd = c.width > 2 && c.width % 4;   // 3, 5, 6, 7, 9, ... bytes: byte loads
+        const uintptr_t need = odd ? 1 : (c.width >= 16 ? 16 : (c.width >= 4 ? 4 : c.width));
         if (reinterpret_cast<uintptr_t>(p) & (need - 1))
             return igx_fail(ctx, IGX_EINVAL, "groupby_update: key column %u misaligned", k);
         a.kcol[k] = p;
@@ -1768,6 +1793,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
             a.kwidth[w] = c.width;
             a.koff[w] = 4 * j;
             a.kmask[w] = c.width >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c.width)) - 1u);
+            a.kbytes[w] = odd ? std::min<uint32_t>(4, c.width - 4 * j) : 0;
         }
     }
     // any readable dword for loads whose result is discarded (padding words, COUNT, no cond)
@@ -1837,16 +1863,48 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         a.vhioff[x] = a.vload[x] && a.vwidth[x] == 8 ? 4 : 0;
         a.chioff[x] = a.cload[x] && a.cwidth[x] == 8 ? 4 : 0;
     }
-    if (npreds > PMAX) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: more than %d predicates", PMAX);
+    // Up to PMAX scalar comparisons (and IN sets) are fused into the kernel; any others --
+    // more predicates, regex or string rules -- are AND-ed into a row mask first by a scan
+    // with the filter's predicate evaluator (k_common.h), which then masks rows like `valid`.
+    std::vector<igx_pred> fused, masked;
+    auto fusable = [&](const igx_pred &q) {
+        const igx_col &c = cols[q.col];
+        return !(q.cmp == IGX_CMP_REGEX || c.kind == IGX_KIND_BYTES || c.kind == IGX_KIND_BOOL ||
+                 c.kind == IGX_KIND_OTHER || (c.width != 1 && c.width != 2 && c.width != 4 && c.width != 8) ||
+                 (c.kind == IGX_KIND_FLOAT && c.width < 4));
+    };
+    for (uint32_t p = 0; p < npreds; ++p) {
+        if (preds[p].col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: predicate column out of range");
+        (fusable(preds[p]) ? fused : masked).push_back(preds[p]);
+    }
+    while (fused.size() > PMAX) {   // overflow into the mask, set tests (IN) last: the mask scan has none
+        auto it = std::find_if(fused.begin(), fused.end(), [](const igx_pred &q) { return q.cmp != IGX_CMP_IN; });
+        if (it == fused.end())
+            return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: more than %d set-membership predicates", PMAX);
+        masked.push_back(*it);
+        fused.erase(it);
+    }
+    if (!masked.empty()) {
+        int rc = grow(ctx, reinterpret_cast<void **>(&t->p_mask), &t->p_mask_bytes, igx_align(nrows, 256));
+        if (rc) return rc;
+        const uint8_t *in = valid;
+        for (size_t b = 0; b < masked.size(); b += IGX_KMAX_PREDS) {
+            DevPreds dp;
+            rc = igx_build_preds(ctx, cols, ncols, masked.data() + b,
+                                 (uint32_t)std::min<size_t>(IGX_KMAX_PREDS, masked.size() - b), &dp);
+            if (rc) return rc;
+            hipLaunchKernelGGL(k_pred_mask, dim3((unsigned)std::min<uint64_t>(4096, (nrows + 255) / 256)), dim3(256), 0,
+                               ctx->stream, dp, in, nrows, t->p_mask);
+            IGX_HIP(ctx, hipGetLastError());
+            in = t->p_mask;
+        }
+        valid = t->p_mask;
+    }
+    preds = fused.data();
+    npreds = (uint32_t)fused.size();
     for (uint32_t p = 0; p < npreds; ++p) {
         const igx_pred &q = preds[p];
-        if (q.col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: predicate column out of range");
         const igx_col &c = cols[q.col];
-        if (q.cmp == IGX_CMP_REGEX || c.kind == IGX_KIND_BYTES || c.kind == IGX_KIND_BOOL ||
-            c.kind == IGX_KIND_OTHER || (c.width != 1 && c.width != 2 && c.width != 4 && c.width != 8) ||
-            (c.kind == IGX_KIND_FLOAT && c.width < 4))
-            return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: predicate %u is not a scalar comparison "
-                                              "(run igx_filter first)", p);
         if (q.cmp == IGX_CMP_IN) {
             if (q.ref_len == 0 || q.ref_len % c.width || q.ref_len > 8 || c.kind == IGX_KIND_FLOAT)
                 return igx_fail(ctx, IGX_EINVAL, "groupby_update: IN predicate %u needs 1..8/width "
@@ -2021,9 +2079,9 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
                                 uint32_t *out_slots) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "groupby_sort: more than 8 keys");
-    igx_sortkey sk[8];
-    uint32_t strides[8];
+    if (nkeys > 32) return igx_fail(ctx, IGX_ENOTSUP, "groupby_sort: more than 32 keys");
+    igx_sortkey sk[32];
+    uint32_t strides[32];
     uint32_t direct = 0;
     for (uint32_t i = 0; i < nkeys; ++i) {
         const igx_tsortkey &q = keys[i];

@@ -27,11 +27,12 @@ namespace {
 constexpr int TB = 256;
 constexpr int IPT = 16;
 constexpr int TILE = TB * IPT;   // 4096 rows per tile
-constexpr int MAXW = 80;          // composed words (<= 8 keys x 64-byte strings + pos + nil)
+constexpr int MAXW = 80;          // composed words (keys + pos + nil; wider keys: ENOTSUP)
+constexpr int NSK = 32;           // sort keys
 
 struct ComposeArgs {
-    const uint8_t *ptr[8];
-    uint32_t width[8], kind[8], desc[8], words[8], rstride[8], direct[8];   // direct: read at i, not rowmap[i]
+    const uint8_t *ptr[NSK];
+    uint32_t width[NSK], kind[NSK], desc[NSK], words[NSK], rstride[NSK], direct[NSK];   // direct: read at i, not rowmap[i]
     uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
     const uint64_t *pos;
     const uint8_t *valid;
@@ -613,7 +614,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride) {
     if (nrows == 0) return IGX_OK;
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
-    if (nkeys > 8) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than 8 keys");
+    if (nkeys > NSK) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than %d keys", NSK);
     ComposeArgs ca{};
     uint32_t KW = valid ? 1 : 0;
     for (uint32_t k = 0; k < nkeys; ++k) {

@@ -56,8 +56,6 @@ def _group_one(cols: Columns, batch: EventBatch, col, all_rows: bool):
         key_idx = cols.index(col.Name)
         t = tensors[key_idx]
         kw = t.shape[1] if t.dim() == 2 else t.element_size()
-    if kw == 3 or (kw > 4 and kw % 4):
-        raise IgxError(_abi.IGX_ENOTSUP, f"group key width {kw}")
     valid = batch.valid
     aggs = []
     for c in sums:

@@ -6,6 +6,7 @@ the advise network-policy tuple, single-column keys, plus l
 no compile-time kernel (generic path).  Bit-exact: keys, every aggregate, first index.
 """
 import ctypes as C
+import re
 
 import numpy as np
 import pytest
@@ -489,5 +490,44 @@ def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, 
     _check(E, H, tab, widths, *o)
     tab.reset()                                            # a second interval, one update
     tab.update(cols, list(range(len(names))), n, 9, valid=dv, idx_col=icol)
+    _check(E, H, tab, widths, *o)
+    tab.destroy()
+
+
+def test_odd_key_widths_and_unfused_predicates(oracle, E, H, igx, torch):
+    """Key columns of 3, 5, 6 and 7 bytes (byte loads in the generic layout, any alignment)
+    and more predicates than the kernel fuses -- a string comparison, a regex and four scalar
+    ones: the extra ones become a device row mask (k_pred_mask, the filter's evaluator)
+    AND-ed with the nil mask.  Exact against the oracle over two chunked updates."""
+    A = igx._abi
+    rng = np.random.default_rng(21)
+    n = 300_000
+    k3 = rng.integers(0, 4, (n, 3)).astype(np.uint8)
+    k5 = rng.integers(0, 3, (n, 5)).astype(np.uint8)
+    k6 = rng.integers(0, 2, (n, 6)).astype(np.uint8)
+    k7 = rng.integers(0, 2, (n, 7)).astype(np.uint8)
+    v = rng.integers(0, 1000, n).astype(np.uint32)
+    p1 = rng.integers(0, 100, n).astype(np.int32)
+    p2 = rng.integers(0, 100, n).astype(np.uint16)
+    names = np.array([b"bash", b"sshd", b"kworker", b"demo"], dtype="S16")
+    comm = np.frombuffer(names[rng.integers(0, 4, n)].tobytes(), np.uint8).reshape(n, 16).copy()
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    cols = [H.to_device(x) for x in (k3, k5, k6, k7, v, p1, p2, comm)]
+    ref = (C.c_uint8 * A.MAX_REF)(*b"s.*d")
+    preds = [_pred(A, 5, A.CMP_GE, 10, np.int32), _pred(A, 5, A.CMP_LT, 90, np.int32),
+             _pred(A, 6, A.CMP_GT, 5, np.uint16), _pred(A, 6, A.CMP_LE, 95, np.uint16, negate=True),
+             A.Pred(7, A.CMP_REGEX, 1, 4, ref),                       # !~s.*d
+             A.Pred(7, A.CMP_EQ, 1, 0, (C.c_uint8 * A.MAX_REF)())]    # string != 
+    comm_s = [bytes(r).split(b"\0")[0].decode() for r in comm]
+    keep = (valid.astype(bool) & (p1 >= 10) & (p1 < 90) & (p2 > 5) & ~(p2 <= 95)
+            & np.array([re.search("s.*d", c) is None for c in comm_s]) & np.array([c != "" for c in comm_s]))
+    widths = [3, 5, 6, 7]
+    tab = E.Table(widths, [A.Agg(A.AGG_SUM, 4, A.NO_COL, 8, 0)], 65536)
+    dv = H.to_device(valid)
+    half = n // 2
+    for a, b in ((0, half), (half, n)):
+        tab.update([c[a:b] for c in cols], [0, 1, 2, 3], b - a, a, preds=preds, valid=dv[a:b])
+    o = oracle.groupby(np.concatenate([k3, k5, k6, k7], axis=1), [{"kind": "sum", "val": v}],
+                       valid=keep.astype(np.uint8))
     _check(E, H, tab, widths, *o)
     tab.destroy()

@@ -289,3 +289,25 @@ def test_float_sort_keys_match_go(oracle, igx, torch):
     got = H.host(E.sort_perm([(H.to_device(bad), True)], n, valid=H.to_device(valid))).astype(np.int64)
     ref = oracle.go_sort_entries([(bad, "float64", True)], n, valid=valid).astype(np.int64)
     assert np.array_equal(got, ref)
+
+
+def test_many_sort_keys(oracle, E, H, torch):
+    """More than 8 sort keys (the composed radix key takes up to 32 keys): 12 narrow keys
+    with heavy ties and mixed directions, exact Go SliceStable order and top-K."""
+    rng = np.random.default_rng(12)
+    n = 20_000
+    kinds = ["int8", "uint16", "string", "int32", "uint8", "int64", "uint32", "int16", "string", "uint64",
+             "int8", "uint8"]
+    keys_d, keys_o = [], []
+    for kd in kinds:
+        desc = bool(rng.random() < 0.5)
+        if kd == "string":
+            a = np.zeros((n, 4), np.uint8)
+            a[:, 0] = rng.integers(97, 99, n)
+        else:
+            a = rng.integers(-1 if kd.startswith("int") else 0, 2, n).astype(kd)
+        keys_d.append((H.to_device(a), desc))
+        keys_o.append((a, kd, desc))
+    ref = oracle.go_sort_entries(keys_o, n)
+    assert np.array_equal(H.host(E.sort_perm(keys_d, n)), ref)
+    assert np.array_equal(H.host(E.sort_perm(keys_d, n, k=50)), ref[:50])
