@@ -144,10 +144,11 @@ int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *fil
                      igx_pred *out, char *errbuf, size_t errlen);
 
 /* Regex rules (IGX_CMP_REGEX, on string columns) run on the device: the pattern is compiled
- * on the host to a DFA over rune classes with Go regexp semantics (RE2 syntax; UTF-8
- * decoded like utf8.DecodeRune; unanchored MatchString).  Syntax it does not compile
- * (\b, \pN, (?m), non-ASCII literals under (?i)) makes igx_filter return IGX_ENOTSUP.
- * igx_regex_compile_blob exposes the compiled automaton (for tests and tools). */
+ * on the host to a DFA over rune classes with Go regexp semantics (RE2 syntax incl. \b \B
+ * \A \z, (?m) (?i) (?s), \p{..} general categories, POSIX classes; UTF-8 decoded like
+ * utf8.DecodeRune; unanchored MatchString).  Script classes (\p{Greek}) are not compiled:
+ * igx_filter returns IGX_ENOTSUP.  igx_regex_compile_blob exposes the compiled automaton
+ * (for tests and tools). */
 int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
                            size_t *out_len, char *errbuf, size_t errlen);
 
@@ -260,13 +261,17 @@ typedef struct {
 } igx_tsortkey;
 
 /* capacity = maximum number of distinct groups.  key_widths: byte width of each key
- * column (packed, each padded to a multiple of 4). */
+ * column, any width (packed, each padded to a multiple of 4; at most IGX_MAX_KEY_BYTES
+ * padded bytes in all).  The table's key records must stay below 4 GiB (S >= 2 x capacity
+ * slots of 32..256 B: about 16M groups for the 72-B ip_key_t), IGX_ENOTSUP otherwise. */
 int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint32_t nkeys,
                        const igx_agg *aggs, uint32_t naggs, uint64_t capacity,
                        igx_table **out);
 /* Aggregate rows [0,nrows) of cols into the table; key_cols selects the key columns
  * (in the table's key order); preds are AND-ed filters applied first (the BPF probe
- * checks).  base_idx is the global index of row 0 (first-occurrence order); indices must
+ * checks): any number, of any kind igx_filter takes plus IGX_CMP_IN sets (up to two scalar
+ * comparisons / sets are fused into the aggregation kernel, the others -- regex, string
+ * rules, more comparisons -- first become a device row mask).  base_idx is the global index of row 0 (first-occurrence order); indices must
  * stay below 2^48 - 1 (IGX_EINVAL otherwise; an index column value at or above it fails the
  * interval at finalize): long-running streams rebase their indices per interval.  Async. */
 int igx_groupby_update(igx_table *t, const igx_col *cols, uint32_t ncols,
@@ -329,6 +334,11 @@ int igx_np_mark(igx_ctx *ctx, const uint8_t *typ, const uint8_t *pkt, const uint
  * ndev == 0 is the shipped gadget's keying (no targ_per_disk / targ_per_flag): every row
  * is device index 0 and dev may be NULL.  cont may be NULL (ncont must then be 1).
  * hist (device u32, max(ndev,1)*ncont*nslots) accumulates.  Async. */
+int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
+                  const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
+                  uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
+
+/* ---- group:sum of float columns, IP text --------------------------------------------- */
 /* GroupEntries' float group:sum (group.go:133-156, flattenValues): perm (device u32, n) is a
  * stable sort of the rows by the group key (key_bytes at row * key_stride of keys); each run
  * of equal keys is one group in input order.  For each run, out[first row of the run] =
@@ -348,10 +358,6 @@ int igx_segment_fsum(igx_ctx *ctx, const uint8_t *keys, uint32_t key_stride, uin
 #define IGX_IPTEXT_WIDTH 40
 int igx_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t addr_stride, const uint8_t *family,
                 uint32_t family_stride, const uint32_t *rowmap, uint64_t n, uint8_t *out);
-
-int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
-                  const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
-                  uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
 
 /* ---- data movement either side of the path ---------------------------------------------- */
 /* Sender side of the group-by all-to-all: rows (device, nrows x
