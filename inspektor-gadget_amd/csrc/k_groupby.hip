@@ -1631,112 +1631,180 @@ static int grow(igx_ctx *ctx, void **p, size_t *have, size_t need) {
     return IGX_OK;
 }
 
-// The partitioned form (k_groupby_part.h): passes A, S, B, I, C.
-template <class L, int NA>
-static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a) {
+// The partitioned form (k_groupby_part.h): passes K, O, S, A, B, C.
+template <class L, int NV>
+static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     constexpr int KW = L::KW;
-    PartArgs p{};
-    // record layout: key words, then the loaded value / condition columns, then the index
-    uint32_t wp = KW;
-    for (uint32_t x = 0; x < t->naggs; ++x) {
-        if (a.vload[x]) {
-            p.vpos[x] = wp;
-            p.vw2[x] = a.vwidth[x] == 8;
-            wp += 1 + p.vw2[x];
-        }
-        if (a.cload[x]) {
-            p.cpos[x] = wp;
-            p.cw2[x] = a.cwidth[x] == 8;
-            wp += 1 + p.cw2[x];
-        }
-    }
-    p.iw = a.fidx ? 2 : 1;
-    p.ipos = wp;
-    wp += p.iw;
-    p.rq = (4 * wp + 15) / 16;
-    // tiles of A and B: as many records (a power of two in [PTS, 4096]) as fit the staging LDS
-    // with their bucket and permutation entries, so that several blocks share a CU
-    const size_t per_rec = 16 * (size_t)p.rq + 4;
-    uint32_t tr = 4096;
-    while (tr > PTS && (size_t)tr * per_rec > PART_TILE_LDS) tr >>= 1;
-    if ((size_t)tr * per_rec > 136 * 1024)
-        return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: rows of %u B are too wide for the partitioned form",
-                        16 * p.rq);
-    p.tr1 = p.tr2 = tr;
-    // final buckets small enough that the expected groups of one (from the table's capacity)
-    // fill at most half of the LDS table; each owns whole probe regions
-    const size_t entry = 8 + 8 * (size_t)t->naggs + 8 + 4 * (size_t)KW;
-    const uint32_t lb_min = t->sbits > 15 ? t->sbits - 15 : 0;   // <= 32K slots per bucket
-    const uint32_t lb_max = std::min<uint32_t>(t->sbits - t->rbits, 28);
+    constexpr uint32_t TRA = PTA * part_rows<KW, NV>();
+    if (4 * p.rq > (uint32_t)part_w<KW, NV>()) return igx_fail(ctx, IGX_EINVAL, "groupby_update: record layout");
+    // final buckets: enough that a bucket's share of the capacity fills at most ~60% of the
+    // C block's LDS table; each bucket owns whole probe regions of the table
+    const size_t entry = agg_entry_bytes(KW, t->naggs);
+    p.uc = p.rq <= 1 ? 2 : 1;
+    const size_t stage_c = (size_t)p.uc * PTC * p.rq * 16;
+    const uint32_t lb_max = std::min<uint32_t>(PART_LB_MAX, t->sbits - t->rbits);
     auto entries = [&](uint32_t lb) {
-        const size_t occw = (size_t)1 << (t->sbits - lb - 5);
-        return (PART_AGG_LDS - 8 * occw - 4 * (2 * PSEG + 1) - 4 * (PT / 64) - 64) / entry;
+        const int64_t occw = (int64_t)1 << (t->sbits - lb - 5);
+        const int64_t room = (int64_t)PART_AGG_LDS - (int64_t)stage_c - 8 * occw - 16;
+        if (room < (int64_t)(8 * entry)) return 0u;
+        return (uint32_t)std::min<int64_t>(65528, room / (int64_t)entry) & ~7u;   // whole 8-way sets
     };
-    uint32_t lb = lb_min;
-    while (lb < lb_max && (t->cap >> lb) * 2 > entries(lb)) ++lb;
+    uint32_t lb = 0;
+    while (lb < lb_max && (double)(t->cap >> lb) > 0.9 * entries(lb)) ++lb;
+    p.lb = lb;
     p.f1 = (lb + 1) / 2;
     p.f2 = lb / 2;
     p.sb_log = t->sbits - lb;
     p.occw = 1u << (p.sb_log - 5);
-    p.E = (uint32_t)entries(lb);
+    p.E = entries(lb);
+    if (p.E < 8) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: key of %u words too wide for the partitioned form", KW);
     if (const char *d = std::getenv("IGX_GBP_ENTRIES"))   // tests: a small LDS table overflows
-        p.E = std::max<uint32_t>(8, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0)));
-    p.maxp = std::min<uint32_t>(p.E, 512);
+        p.E = std::max<uint32_t>(8, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0))) & ~7u;
+    p.maxp = std::min<uint32_t>(p.E / 8, 32);   // sets probed before a row takes the HBM path
+    p.combine = 0;   // wave pre-combine: measured slower on C4 and C5
+    if (const char *d = std::getenv("IGX_GBP_COMBINE")) p.combine = (uint32_t)std::strtoul(d, nullptr, 0);
     if (const char *d = std::getenv("IGX_GBP_DEBUG")) p.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
-    const uint32_t F1 = 1u << p.f1, F2 = 1u << p.f2, nb = 1u << lb;
-    p.ch = (uint32_t)std::max<uint64_t>(16384, 4 * (a.n / nb + 1));
-    p.tiles1 = (uint32_t)((a.n + p.tr1 - 1) / p.tr1);
-    p.tiles2max = (uint32_t)((a.n + p.tr2 - 1) / p.tr2) + F1;
-    // scratch: h1 | p1 | base1 | t2base | h2 | items (u32 words), records of A and B
-    const uint64_t w_h1 = (uint64_t)p.tiles1 * (F1 + 1), w_p1 = (uint64_t)F1 * (p.tiles1 + 1);
-    const uint64_t w_h2 = (uint64_t)p.tiles2max * (F2 + 1);
-    p.imax = (uint32_t)std::min<uint64_t>(0xFFFFFFFFu, 2ull * nb + a.n / p.ch + 2);
-    const uint64_t words = w_h1 + w_p1 + 2 * (F1 + 1) + w_h2 + nb + 1 + 3ull * p.tiles2max + p.imax;
-    const size_t rec_bytes = (size_t)16 * p.rq;
+    const uint32_t F1 = 1u << p.f1, F2 = 1u << p.f2, NB = 1u << lb;
+    // B tiles: as many records (a multiple of PTA, at most 4096) as the tile LDS holds
+    uint32_t trb = 4096;
+    while (trb > PTA && (size_t)trb * (16 * p.rq + 6) + 12 * PART_F_MAX + 72 > PART_TILE_LDS) trb -= PTA;
+    p.trb = trb;
+    p.ch = (uint32_t)std::max<uint64_t>(8192, 4 * (a.n / NB + 1));
+    p.tiles_a = (uint32_t)((a.n + TRA - 1) / TRA);
+    p.nchunk = (p.tiles_a + CHT - 1) / CHT;
+    const uint64_t tiles_b = a.n / trb + F1 + 1;
+    const uint64_t items_max = NB + a.n / p.ch + 1;
+    // scratch: cnt1 | csum | hist | start2 | cur2 | tstart | bt | istart | itfb | ctl (u32 words)
+    const uint64_t w_cnt1 = (uint64_t)p.tiles_a * F1, w_csum = (uint64_t)p.nchunk * F1;
+    const uint64_t words = w_cnt1 + w_csum + NB + (NB + 1) + NB + (F1 + 1) + tiles_b + (NB + 1) + items_max + 4;
     int rc = grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
-    if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes,
-                       rec_bytes * ((uint64_t)p.tiles1 * p.tr1 + a.n));
+    const size_t rec_bytes = (size_t)16 * p.rq;
+    if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes, 2 * rec_bytes * a.n);
     if (rc) return rc;
-    p.h1 = t->p_cnt;
-    p.p1 = p.h1 + w_h1;
-    p.base1 = p.p1 + w_p1;
-    p.t2base = p.base1 + F1 + 1;
-    p.h2 = p.t2base + F1 + 1;
-    p.items = p.h2 + w_h2;
-    p.bmap = p.items + nb + 1;
-    p.imap = p.bmap + 3ull * p.tiles2max;
+    p.cnt1 = t->p_cnt;
+    p.csum = p.cnt1 + w_cnt1;
+    p.hist = p.csum + w_csum;
+    p.start2 = p.hist + NB;
+    p.cur2 = p.start2 + NB + 1;
+    p.tstart = p.cur2 + NB;
+    p.bt = p.tstart + F1 + 1;
+    p.istart = p.bt + tiles_b;
+    p.itfb = p.istart + NB + 1;
+    p.ctl = p.itfb + items_max;
     p.recs1 = t->p_recs;
-    p.recs2 = t->p_recs + (uint64_t)p.tiles1 * p.tr1 * p.rq * 4;
-    const size_t lds_a = (size_t)p.tr1 * (rec_bytes + 4) + 4 * (F1 + 1) + 4 * 17;
-    const size_t lds_b = (size_t)p.tr2 * (rec_bytes + 4) + 4 * (F2 + 1) + 4 * 17 + 4 * (2 * PSEGB + 1) + p.tr2 / 16;
-    const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 4 * (2 * PSEG + 1) + 4 * (PT / 64) + 64;
-    static size_t lds_set[3] = {0, 0, 0};   // dynamic LDS granted to each kernel so far
-    const void *kern[3] = {reinterpret_cast<const void *>(k_gbp_a<L, NA>),
-                           reinterpret_cast<const void *>(k_gbp_b<KW, NA>),
-                           reinterpret_cast<const void *>(k_gbp_c<KW, NA>)};
-    const size_t need[3] = {lds_a, lds_b, lds_c};
-    for (int i = 0; i < 3; ++i) {
+    p.recs2 = t->p_recs + (uint64_t)a.n * p.rq * 4;
+    const size_t lds_k = 4 * ((size_t)NB + F1);
+    const size_t lds_a = (size_t)TRA * (16 * p.rq + 1) + 12 * (size_t)F1 + 4 * 17;
+    const size_t lds_b = (size_t)trb * (16 * p.rq + 6) + 12 * (size_t)F2 + 4 * 17;
+    const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 16 + stage_c;
+    static size_t lds_set[4] = {0, 0, 0, 0};   // dynamic LDS granted to each kernel so far
+    const void *kern[4] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
+                           reinterpret_cast<const void *>(k_gbp_a<L, NV>),
+                           reinterpret_cast<const void *>(k_gbp_b<KW, NV>),
+                           reinterpret_cast<const void *>(k_gbp_c<KW, NV>)};
+    const size_t need[4] = {lds_k, lds_a, lds_b, lds_c};
+    for (int i = 0; i < 4; ++i) {
         if (need[i] > lds_set[i]) {
             IGX_HIP(ctx, hipFuncSetAttribute(kern[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[i]));
             lds_set[i] = need[i];
         }
     }
-    hipLaunchKernelGGL((k_gbp_a<L, NA>), dim3(p.tiles1), dim3(PTS), lds_a, ctx->stream, a, p);
-    hipLaunchKernelGGL(k_gbp_colscan, dim3(F1), dim3(1024), 0, ctx->stream, p);
-    hipLaunchKernelGGL(k_gbp_base, dim3(1), dim3(1024), 0, ctx->stream, p);
-    hipLaunchKernelGGL(k_gbp_bmap, dim3((p.tiles2max + 255) / 256), dim3(256), 0, ctx->stream, p);
-    hipLaunchKernelGGL((k_gbp_b<KW, NA>), dim3(p.tiles2max), dim3(PTS), lds_b, ctx->stream, p);
-    hipLaunchKernelGGL(k_gbp_icount, dim3(F1), dim3(256), 0, ctx->stream, p);
-    hipLaunchKernelGGL(k_gbp_iscan, dim3(1), dim3(1024), 0, ctx->stream, p);
-    hipLaunchKernelGGL(k_gbp_imap, dim3(256), dim3(256), 0, ctx->stream, p);
-    hipLaunchKernelGGL((k_gbp_c<KW, NA>), dim3((unsigned)ctx->num_cus), dim3(PT), lds_c, ctx->stream, a, p);
+    const uint32_t cus = (uint32_t)ctx->num_cus;
+    IGX_HIP(ctx, hipMemsetAsync(p.hist, 0, 4ull * NB, ctx->stream));
+    hipLaunchKernelGGL((k_gbp_count<L, NV>), dim3(std::min<uint32_t>(p.tiles_a, 2 * cus)), dim3(PTA), lds_k,
+                       ctx->stream, a, p);
+    hipLaunchKernelGGL(k_gbp_csum, dim3(p.nchunk), dim3(PTA), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_scan, dim3(1), dim3(1024), 0, ctx->stream, p);
+    hipLaunchKernelGGL(k_gbp_offs, dim3(p.nchunk), dim3(PTA), 0, ctx->stream, p);
+    if (p.dbg & 1024u) return IGX_OK;   // diagnostics: stop after the count and the scans
+    hipLaunchKernelGGL((k_gbp_a<L, NV>), dim3(p.tiles_a), dim3(PTA), lds_a, ctx->stream, a, p);
+    if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
+    hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
+    if (p.dbg & 512u) return IGX_OK;   // ... after pass B
+    hipLaunchKernelGGL((k_gbp_c<KW, NV>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     return IGX_OK;
 }
 
+// record layout and the loaded columns; predicates become a row mask first
 template <class L>
 static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
-    if (a.naggs <= 2) return launch_part_as<L, 2>(t, ctx, a);
-    return launch_part_as<L, AMAX>(t, ctx, a);
+    PartArgs p{};
+    // packed key words: 1- and 2-byte columns share words, other columns keep theirs
+    uint32_t wp = 0, used = 4, shared = 0, w = 0;
+    for (uint32_t c = 0; c < t->nkeys; ++c) {
+        const uint32_t cw = t->key_widths[c];
+        if (cw <= 2) {
+            if (used + cw > 4) {
+                shared = wp++;
+                used = 0;
+            }
+            p.kpw[w] = shared;
+            p.ksh[w] = 8 * used;
+            p.kmsk[w] = cw == 1 ? 0xFFu : 0xFFFFu;
+            used += cw;
+            ++w;
+        } else {
+            for (uint32_t j = 0; j < (cw + 3) / 4; ++j, ++w) {
+                p.kpw[w] = wp++;
+                p.ksh[w] = 0;
+                p.kmsk[w] = 0xFFFFFFFFu;
+            }
+        }
+    }
+    if (w != t->key_words) return igx_fail(ctx, IGX_EINVAL, "groupby_update: internal key packing mismatch");
+    p.kpn = wp;
+    // each distinct value / condition column once
+    uint32_t nv = 0;
+    auto col_of = [&](const uint8_t *ptr, uint32_t width) {
+        for (uint32_t j = 0; j < nv; ++j)
+            if (p.vcol[j] == ptr && p.vcw[j] == width) return j;
+        p.vcol[nv] = ptr;
+        p.vcw[nv] = width;
+        p.vchi[nv] = width == 8 ? 4 : 0;
+        return nv++;
+    };
+    for (uint32_t x = 0; x < AMAX; ++x) {
+        p.vsrc[x] = p.csrc[x] = PNV;
+        if (x >= t->naggs) continue;
+        if (!a.vcount[x]) p.vsrc[x] = col_of(a.vptr[x], a.vwidth[x]);
+        if (a.hascond[x]) p.csrc[x] = col_of(a.cptr[x], a.cwidth[x]);
+    }
+    for (uint32_t j = 0; j < nv; ++j) {
+        p.rpos[j] = wp;
+        p.rw2[j] = p.vcw[j] == 8;
+        wp += 1 + p.rw2[j];
+    }
+    p.nv = nv;
+    for (uint32_t x = 0; x < AMAX; ++x) {
+        p.avp[x] = p.vsrc[x] < PNV ? p.rpos[p.vsrc[x]] : 0xFFFFu;
+        p.av2[x] = p.vsrc[x] < PNV ? p.rw2[p.vsrc[x]] : 0u;
+        p.acp[x] = p.csrc[x] < PNV ? p.rpos[p.csrc[x]] : 0xFFFFu;
+        p.ac2[x] = p.csrc[x] < PNV ? p.rw2[p.csrc[x]] : 0u;
+    }
+    for (uint32_t j = nv; j < PNV; ++j) {   // unused: dword 0 of a readable column
+        p.vcol[j] = a.kcol[0];
+        p.vcw[j] = 0;
+        p.vchi[j] = 0;
+        p.rpos[j] = 0;
+        p.rw2[j] = 0;
+    }
+    p.iw = a.fidx ? 2 : 1;
+    p.ipos = wp;
+    wp += p.iw;
+    p.rq = (wp + 3) / 4;
+    p.rq_magic = p.rq > 1 ? (uint32_t)((0x100000000ull + p.rq - 1) / p.rq) : 0u;
+    if (a.npred) {
+        int rc = grow(ctx, reinterpret_cast<void **>(&t->p_mask), &t->p_mask_bytes, igx_align(a.n, 256));
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_gbp_mask, dim3((unsigned)std::min<uint64_t>(4096, (a.n + 255) / 256)), dim3(256), 0,
+                           ctx->stream, a, t->p_mask);
+        a.valid = a.validp = t->p_mask;
+        a.validw = 1;
+        a.npred = 0;
+    }
+    if (nv == 0) return launch_part_as<L, 0>(t, ctx, a, p);
+    if (nv <= 2) return launch_part_as<L, 2>(t, ctx, a, p);
+    return launch_part_as<L, PNV>(t, ctx, a, p);
 }
 
 // one update over layout L in the interval's form
@@ -1976,6 +2044,12 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     }
     if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = t->interval_part = false;   // diagnostics: cached form
     int rc = IGX_OK;
+#ifdef IGX_DEV_FAST   // development builds: the bench's key layouts only (fast kernel iteration)
+    if (layout_is<TcpKey>(kw, t->nkeys)) rc = launch_form<TcpKey>(t, ctx, a, blocks);
+    else if (layout_is<FileKey>(kw, t->nkeys)) rc = launch_form<FileKey>(t, ctx, a, blocks);
+    else if (layout_is<NetPolicyKey>(kw, t->nkeys)) rc = launch_form<NetPolicyKey>(t, ctx, a, blocks);
+    else return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: layout not in this development build");
+#else
     if (t->generic) {
         switch (t->kw_rec) {
         case 2: rc = launch_form<GenericLayout<2>>(t, ctx, a, blocks); break;
@@ -1999,6 +2073,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     else if (t->nkeys == 1 && kw[0] == 8) rc = launch_form<StaticLayout<8>>(t, ctx, a, blocks);
     else if (t->nkeys == 1 && kw[0] == 16) rc = launch_form<StaticLayout<16>>(t, ctx, a, blocks);
     else return igx_fail(ctx, IGX_EINVAL, "groupby_update: internal layout mismatch");
+#endif
     if (rc) return rc;
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;

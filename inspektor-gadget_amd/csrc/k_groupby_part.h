@@ -6,131 +6,167 @@
 // first-event-wins map, advisor.go:279-320): exact keys, wrapped sums, first event index.
 //
 // Near-uniform streams with millions of distinct keys (C4's network-policy tuples, C5's
-// 10M files) miss any per-CU cache, and the cached / direct forms then pay one random HBM
-// probe (plus memory-side atomics) per row -- the chip's small-random-access rate (~40 G/s)
-// bounds them.  A one-level scatter into thousands of buckets does no better: its record
-// writes are just as random.  This form is a two-level radix partition in which every
-// per-row HBM access is streamed and coalesced:
-//   A  a block reads a tile of rows, packs the kept ones into records (key words | raw value
-//      / condition column values | index) in LDS, sorts them there by the hash's top f1
-//      bits (counting sort) and writes the sorted tile contiguously with its bucket offsets;
-//   S  per first-level bucket b1: a scan of its counts over the A tiles, b1's start in the
-//      B output and its first B tile;
-//   B  a block gathers tr2 consecutive records of b1 (its segments of the A tiles), sorts
-//      them by the next f2 bits and writes them contiguously (b1's records stay together);
-//   I  per final bucket (b1, b2): its records over b1's B tiles -> aggregate work items;
-//   C  an item builds its final bucket's groups in an LDS hash table (full key compare, u64
-//      sums, min first index) from the bucket's segments of the B tiles, then writes them to
-//      the HBM table.  A final bucket owns whole probe regions of the table (home slot = the
-//      hash's top bits, probing wraps inside a region), so an item that is its bucket's only
-//      one writes its groups with plain loads and stores -- no CAS, no atomics, occupancy
-//      bits through an LDS copy of the bucket's bitmap words.  Items of a split bucket (skew)
-//      and rows that overflow the LDS table merge with the table's CAS claims and atomics.
-// HBM bytes per kept row: the input read once, then one record written and read back twice;
-// per group one probe of its home region.
+// 10M files) miss any per-CU cache, and a form that probes the HBM table per row is bound by
+// the chip's small-random-access rate (~50-60 G requests/s whatever the table size,
+// tools/micro/randacc.hip).  This form turns every per-row access into a streamed one: the
+// rows are radix-partitioned by the key hash into NB = 2^lb final buckets in two scatter
+// passes, and each final bucket is then aggregated in LDS by one workgroup.
+//   K  count, with pass A's tiling: rows per final bucket (the hash's top lb bits) and per
+//      (A tile, first-level bucket) (the top f1 bits);
+//   O  chunk sums and exclusive offsets of the per-tile counts: each A tile's exact output
+//      position per first-level bucket (no atomics in pass A);
+//   S  one block: bucket starts, pass B's cursors and tiles, pass C's work items;
+//   A  a tile of rows -> records (packed key words | raw loaded columns | index), ranked in
+//      LDS by the top f1 hash bits and staged sorted; each first-level bucket's run is
+//      written at its exact position: first-level buckets come out contiguous;
+//   B  a tile of one first-level bucket's records, sorted in LDS by the next f2 bits; each
+//      final bucket's run is written at a cursor reserved with one atomic per (tile,
+//      bucket): final buckets come out contiguous;
+//   C  a work item = a final bucket (or a slice of a skewed one): its records are read in
+//      order, pre-combined within each wave64 (the leader's key collects its duplicates'
+//      values with ballot + shuffle), aggregated in an LDS hash table (full key compare, u64
+//      sums, min first index), then written to the HBM table.  A final bucket owns whole
+//      probe regions of the table (home slot = the hash's top bits; probing wraps inside a
+//      region), so an item that is its bucket's only one writes its groups with plain loads
+//      and stores.  Slices of a split bucket, and rows that overflow the LDS table, merge with
+//      the table's CAS claims and atomics.
+// HBM bytes per kept row: the key columns read twice (K, A), the loaded columns once, and
+// one record written and read back twice (A -> B -> C); per group one probe of its region.
 
-constexpr uint32_t PT = 1024;                  // threads per block of the aggregate pass
-constexpr uint32_t PTS = 256;                  // ... of passes A and B (several blocks per CU, so one
-                                               // block's loads overlap another's sort and writes)
-constexpr size_t PART_TILE_LDS = 40 * 1024;    // an A / B tile (records + 4 B each): 4 blocks per CU
-constexpr size_t PART_AGG_LDS = 152 * 1024;
-constexpr uint32_t PSEG = 1024;                // segments a C block maps (B tiles of its bucket)
-constexpr uint32_t PSEGB = 256;                // segments a B block maps at a time (A tiles)
+constexpr uint32_t PTA = 256;                  // threads per block of passes K, A and B
+constexpr uint32_t PTC = 512;                  // ... of the aggregate pass (two blocks per CU)
+constexpr size_t PART_TILE_LDS = 72 * 1024;    // a B tile: records + 6 B each
+constexpr size_t PART_AGG_LDS = 80 * 1024;     // the C block: LDS table + one round of records
+constexpr uint32_t PART_LB_MAX = 15;           // final buckets <= 2^15 (count-pass LDS histogram)
+constexpr uint32_t PART_F_MAX = 256;           // buckets per scatter level (one per thread)
+constexpr uint32_t PNV = 2 * AMAX;             // distinct value / condition columns a record carries
+constexpr uint32_t CHT = 64;                   // A tiles per chunk of the offset scan
 
 struct PartArgs {
-    uint32_t *recs1, *recs2;   // A / B tiles (rq x 16 B per record)
-    uint32_t *h1;              // tiles1 x (F1 + 1): bucket offsets inside each A tile
-    uint32_t *p1;              // F1 x (tiles1 + 1): prefix of b1's records over the A tiles
-    uint32_t *base1;           // F1 + 1: start of b1 in recs2
-    uint32_t *t2base;          // F1 + 1: first B tile of b1
-    uint32_t *h2;              // tiles2max x (F2 + 1): bucket offsets inside each B tile
-    uint32_t *items;           // F1 * F2 + 1: prefix of the aggregate work items per final bucket
-    uint32_t *bmap;            // tiles2max x 3: a B tile's b1, first and last A tile (k_gbp_bmap)
-    uint32_t *imap;            // aggregate work item -> final bucket (k_gbp_imap)
-    uint32_t imax;             // imap entries
-    uint32_t tiles1, tiles2max;
-    uint32_t tr1, tr2;         // record slots of an A / B tile
-    uint32_t f1, f2;           // bucket bits of the two levels
+    uint32_t *recs1, *recs2;   // records after pass A / pass B (rq quads each)
+    uint32_t *cnt1;            // tiles_a x F1: an A tile's rows per first-level bucket, then the
+                               // exact output position of that run (pass O)
+    uint32_t *csum;            // nchunk x F1: the same per chunk of CHT A tiles
+    uint32_t *hist;            // NB: rows per final bucket (pass K)
+    uint32_t *start2;          // NB + 1: first record of each final bucket (prefix of hist)
+    uint32_t *cur2;            // NB: pass B's write cursors (final buckets)
+    uint32_t *tstart;          // F1 + 1: first B tile of each first-level bucket
+    uint32_t *bt;              // B tile -> first-level bucket
+    uint32_t *istart;          // NB + 1: first C work item of each final bucket
+    uint32_t *itfb;            // C work item -> final bucket
+    uint32_t *ctl;             // [0] C work-item dequeue, [1] B tiles, [2] C work items
+    // the row's value / condition columns, each loaded once (aggregates sharing a column
+    // share it): pointer, width (0 = unused: dword 0 of a readable column) and high-dword
+    // offset (4 for 8-byte columns)
+    const uint8_t *vcol[PNV];
+    uint32_t vcw[PNV], vchi[PNV];
+    uint32_t rpos[PNV], rw2[PNV];      // record word of column j's raw value (+1 when 8 bytes)
+    uint32_t nv;                       // loaded columns
+    uint32_t vsrc[AMAX], csrc[AMAX];   // column of aggregate x's value / condition (PNV = none)
+    uint32_t avp[AMAX], acp[AMAX];     // ... its record word (0xFFFF = none) ...
+    uint32_t av2[AMAX], ac2[AMAX];     // ... and 1 when it is 8 bytes wide
+    uint32_t tiles_a, nchunk;  // A tiles (PTA x rows-per-thread rows each), chunks of CHT tiles
+    uint32_t trb;              // records per B tile
+    uint32_t f1, f2, lb;       // bucket bits of the two levels, lb = f1 + f2
     uint32_t sb_log;           // log2 table slots per final bucket
     uint32_t occw;             // occupancy bitmap words per final bucket (slots / 32)
-    uint32_t rq;               // record quads (16 B)
-    uint32_t iw;               // index words: 1 = row offset (gidx = base_idx + row), 2 = global index
-    uint32_t ipos;             // record word of the index
-    uint32_t vpos[AMAX], cpos[AMAX];   // record word of a stored value / condition column (0 = none)
-    uint32_t vw2[AMAX], cw2[AMAX];     // 1: that column is 8 bytes wide (two words)
-    uint32_t ch;               // records per aggregate work item (larger buckets are split)
+    uint32_t rq, rq_magic;     // record quads (16 B); ceil(2^32 / rq) for quad -> record
+    uint32_t kpw[KWMAX];       // key word w lives in record word kpw[w] ...
+    uint32_t ksh[KWMAX];       // ... at this bit shift (1- and 2-byte columns share words)
+    uint32_t kmsk[KWMAX];      // ... with this mask (0 = a padding word)
+    uint32_t kpn;              // packed key words
+    uint32_t iw, ipos;         // index words (1 = row offset, 2 = global index column) and their word
+    uint32_t ch;               // records per C work item (larger buckets are split)
     uint32_t E;                // LDS table entries
+    uint32_t uc;               // records per thread and round of pass C
     uint32_t maxp;             // LDS probes before a row takes the HBM path
+    uint32_t combine;          // wave pre-combine rounds per 64 records (0 = off)
     uint32_t dbg;              // diagnostics (IGX_GBP_DEBUG): phases to skip, results invalid
 };
 
-// record words: key words, then the stored raw columns and the index at host-chosen words
-template <int KW, int NA>
-struct PartRec {
-    static constexpr int W = (KW + 4 * NA + 2 + 3) & ~3;
-    static constexpr int U = W <= 32 ? 2 : 1;   // records in flight per thread
+// record words (compile-time bound): packed key words, loaded columns, index
+template <int KW, int NV>
+constexpr int part_w() { return (KW + 2 * NV + 2 + 3) & ~3; }
+// rows per thread of passes K and A (a row's loaded dwords stay in registers)
+template <int KW, int NV>
+constexpr int part_rows() { return KW + 1 + 2 * NV <= 8 ? 8 : 4; }
+
+// a row's loads: nil mask, key columns, the loaded value / condition columns, index column
+template <class L, int NV>
+struct PRow {
+    uint32_t k[L::KW];
+    uint32_t vraw;
+    uint32_t lo[NV > 0 ? NV : 1], hi[NV > 0 ? NV : 1];
+    uint64_t fi;
 };
 
-template <int KW, int NA>
-__device__ __forceinline__ void rec_pack(const PartArgs &p, const uint32_t (&k)[KW], const uint64_t (&rv)[NA],
-                                         const uint64_t (&rc)[NA], uint64_t idx, uint32_t (&w)[PartRec<KW, NA>::W]) {
-    constexpr int W = PartRec<KW, NA>::W;
+template <class L, int NV, bool VALS>
+__device__ __forceinline__ void prow_issue(const GbArgs &a, const PartArgs &p, uint64_t row, PRow<L, NV> &R) {
+    R.vraw = ldd(a.validp, row * a.validw);
+    L::load(a, row, R.k);
+    if constexpr (VALS) {
 #pragma unroll
-    for (int i = 0; i < W; ++i) {
-        uint32_t x = 0;
-        if (i < KW) {
-            x = k[i];
-        } else {
-            const uint32_t u = (uint32_t)i;
-#pragma unroll
-            for (int c = 0; c < NA; ++c) {
-                if (p.vpos[c] == u) x = (uint32_t)rv[c];
-                if (p.vw2[c] && p.vpos[c] + 1 == u) x = (uint32_t)(rv[c] >> 32);
-                if (p.cpos[c] == u) x = (uint32_t)rc[c];
-                if (p.cw2[c] && p.cpos[c] + 1 == u) x = (uint32_t)(rc[c] >> 32);
-            }
-            if (p.ipos == u) x = (uint32_t)idx;
-            if (p.iw == 2 && p.ipos + 1 == u) x = (uint32_t)(idx >> 32);
+        for (int j = 0; j < NV; ++j) {
+            const uint64_t b = row * p.vcw[j];
+            R.lo[j] = ldd(p.vcol[j], b);
+            R.hi[j] = ldd(p.vcol[j], b + p.vchi[j]);
         }
-        w[i] = x;
+        R.fi = a.fidx ? a.fidx[row] : row;
     }
 }
 
-template <int W>
-__device__ __forceinline__ void recs_load(const uint32_t *recs, uint64_t pos, uint32_t rq, uint32_t (&w)[W]) {
-    const u4v *src = reinterpret_cast<const u4v *>(recs) + pos * rq;
-#pragma unroll
-    for (int q = 0; q < W / 4; ++q) {
-        u4v t = {0, 0, 0, 0};
-        if ((uint32_t)q < rq) t = __builtin_nontemporal_load(src + q);
-        w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
-    }
+template <class L, int NV>
+__device__ __forceinline__ bool prow_ok(const GbArgs &a, uint64_t row, const PRow<L, NV> &R) {
+    return !a.valid || ((R.vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
 }
 
-template <int KW, int NA>
-__device__ __forceinline__ void rec_decode(const GbArgs &a, const PartArgs &p, const uint32_t (&w)[PartRec<KW, NA>::W],
-                                           uint32_t (&k)[KW], uint64_t (&v)[NA], uint64_t &gidx) {
-    constexpr int W = PartRec<KW, NA>::W;
+// A record lives in LDS as rq x 4 words while it is built or read: its fields sit at
+// runtime word offsets (host-chosen layout), so LDS addressing does the packing and no
+// register array is indexed by a runtime value.
+template <class L, int NV>
+__device__ __forceinline__ void prow_stage(const PartArgs &p, uint64_t row, const PRow<L, NV> &R, uint32_t *rec) {
+    constexpr int KW = L::KW;
+    for (uint32_t q = 0; q < p.rq; ++q) reinterpret_cast<uint4 *>(rec)[q] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < KW; ++i) k[i] = w[i];
-    uint64_t rv[NA], rc[NA], idx = 0;
+    for (int j = 0; j < KW; ++j)
+        if (p.kmsk[j]) atomicOr(rec + p.kpw[j], (R.k[j] & p.kmsk[j]) << p.ksh[j]);
 #pragma unroll
-    for (int c = 0; c < NA; ++c) rv[c] = rc[c] = 0;
-#pragma unroll
-    for (int i = KW; i < W; ++i) {
-        const uint32_t u = (uint32_t)i;
-#pragma unroll
-        for (int c = 0; c < NA; ++c) {
-            if (p.vpos[c] == u) rv[c] |= w[i];
-            if (p.vw2[c] && p.vpos[c] + 1 == u) rv[c] |= (uint64_t)w[i] << 32;
-            if (p.cpos[c] == u) rc[c] |= w[i];
-            if (p.cw2[c] && p.cpos[c] + 1 == u) rc[c] |= (uint64_t)w[i] << 32;
+    for (int j = 0; j < NV; ++j) {
+        if ((uint32_t)j < p.nv) {
+            const uint64_t raw = assemble(R.lo[j], R.hi[j], row * p.vcw[j], p.vcw[j]);
+            rec[p.rpos[j]] = (uint32_t)raw;
+            if (p.rw2[j]) rec[p.rpos[j] + 1] = (uint32_t)(raw >> 32);
         }
-        if (p.ipos == u) idx |= w[i];
-        if (p.iw == 2 && p.ipos + 1 == u) idx |= (uint64_t)w[i] << 32;
     }
-    share_raw<NA>(a, rv, rc);
-    vals_from_raw<NA>(a, rv, rc, v);
+    rec[p.ipos] = (uint32_t)R.fi;
+    if (p.iw == 2) rec[p.ipos + 1] = (uint32_t)(R.fi >> 32);
+}
+
+// the table's key words back from a record in LDS
+template <int KW>
+__device__ __forceinline__ void lds_key(const PartArgs &p, const uint32_t *rec, uint32_t (&k)[KW]) {
+#pragma unroll
+    for (int j = 0; j < KW; ++j) k[j] = p.kmsk[j] ? (rec[p.kpw[j]] >> p.ksh[j]) & p.kmsk[j] : 0u;
+}
+
+__device__ __forceinline__ uint64_t lds_field(const uint32_t *rec, uint32_t pos, uint32_t w2) {
+    if (pos == 0xFFFFu) return 0;
+    return (uint64_t)rec[pos] | (w2 ? (uint64_t)rec[pos + 1] << 32 : 0ull);
+}
+
+// a record in LDS -> key words, the values its aggregates add, its global event index
+template <int KW>
+__device__ __forceinline__ void lds_decode(const GbArgs &a, const PartArgs &p, const uint32_t *rec, uint32_t (&k)[KW],
+                                           uint64_t (&v)[AMAX], uint64_t &gidx) {
+    lds_key<KW>(p, rec, k);
+    uint64_t rv[AMAX], rc[AMAX];
+#pragma unroll
+    for (int x = 0; x < AMAX; ++x) {
+        rv[x] = lds_field(rec, p.avp[x], p.av2[x]);
+        rc[x] = lds_field(rec, p.acp[x], p.ac2[x]);
+    }
+    vals_from_raw<AMAX>(a, rv, rc, v);
+    const uint64_t idx = lds_field(rec, p.ipos, p.iw == 2);
     gidx = p.iw == 2 ? idx : a.base_idx + idx;
 }
 
@@ -165,176 +201,82 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wsum, 
     return r;
 }
 
-// ---- passes A and B: a tile sorted in LDS, written in order --------------------------------
-struct TileLds {
-    uint4 *stage;        // tr x rq quads: records in staging order
-    uint16_t *bkt;       // tr: bucket of each staged record
-    uint16_t *perm;      // tr: sorted position -> staged record
-    uint32_t *hist;      // F + 1
-    uint32_t *wsum;      // 17
-};
-
-__device__ __forceinline__ TileLds tile_lds(uint8_t *lds, uint32_t tr, uint32_t rq, uint32_t F) {
-    TileLds L;
-    L.stage = reinterpret_cast<uint4 *>(lds);
-    L.bkt = reinterpret_cast<uint16_t *>(lds + (size_t)tr * rq * 16);
-    L.perm = L.bkt + tr;
-    L.hist = reinterpret_cast<uint32_t *>(L.perm + tr);
-    L.wsum = L.hist + F + 1;
-    return L;
-}
-
-// `cnt` staged records (hist holds their bucket counts) -> dst in bucket order, the tile's
-// bucket offsets (F + 1 words) -> hout.  Order inside a bucket is free (sums commute, the
-// first index is a minimum), so ranks come from LDS atomics; the permutation is built in
-// LDS so that the HBM writes are the tile in order, 16 B per lane.
-__device__ __forceinline__ void tile_sort_write(const TileLds &L, uint32_t cnt, uint32_t F, uint32_t rq,
-                                                uint4 *dst, uint32_t *hout) {
-    const uint32_t bt = blockDim.x;
-    const uint32_t per = (F + bt - 1) / bt;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t b = threadIdx.x * per + i;
-        s += b < F ? L.hist[b] : 0u;
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, L.wsum, total);
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t b = threadIdx.x * per + i;
-        if (b < F) {
-            const uint32_t c = L.hist[b];
-            L.hist[b] = run;
-            hout[b] = run;
-            run += c;
-        }
-    }
-    if (threadIdx.x == 0) hout[F] = total;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += bt) L.perm[atomicAdd(&L.hist[L.bkt[i]], 1u)] = (uint16_t)i;
-    __syncthreads();
-    const uint32_t nq = cnt * rq;
-    for (uint32_t qi = threadIdx.x; qi < nq; qi += bt) {
-        const uint32_t j = qi / rq, q = qi - j * rq;
-        dst[qi] = L.stage[(uint32_t)L.perm[j] * rq + q];
+// Fused predicates of an update in the partitioned form: evaluated once into a row mask
+// (AND-ed with the nil mask), which the passes then read like `valid`.
+__global__ __launch_bounds__(256) void k_gbp_mask(GbArgs a, uint8_t *out) {
+    for (uint64_t row = (uint64_t)blockIdx.x * 256 + threadIdx.x; row < a.n; row += (uint64_t)gridDim.x * 256) {
+        bool ok = !a.valid || a.valid[row] != 0;
+        for (uint32_t q = 0; q < a.npred && q < PMAX; ++q)
+            ok = ok && pred_scalar(ld_val(a.pptr[q], row, a.pwidth[q]), a.pref[q], a.pwidth[q], a.pkind[q], a.pcmp[q],
+                                   a.pneg[q], a.pcnt[q]);
+        out[row] = ok ? 1 : 0;
     }
 }
 
-// A: rows [tile * tr1, ...) -> records sorted by the hash's top f1 bits.  The tile is read
-// in rounds of RA x PTS rows, the next round's loads issued before the current one is packed.
-template <class L, int NA>
-__global__ __launch_bounds__(PTS) void k_gbp_a(GbArgs a, PartArgs p) {
+// ---- K: rows per final bucket, and per (A tile, first-level bucket) -------------------------
+// Same tiling as pass A (PTA x R rows per tile), one block per tile.
+template <class L, int NV>
+__global__ __launch_bounds__(PTA) void k_gbp_count(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
-    constexpr int W = PartRec<KW, NA>::W;
-    extern __shared__ uint8_t lds_raw[];
-    const uint32_t F = 1u << p.f1;
-    const TileLds T = tile_lds(lds_raw, p.tr1, p.rq, F);
-    __shared__ uint32_t cnt_s;
-    for (uint32_t b = threadIdx.x; b < F; b += PTS) T.hist[b] = 0;
-    if (threadIdx.x == 0) cnt_s = 0;
-    __syncthreads();
-    const uint64_t r0 = (uint64_t)blockIdx.x * p.tr1;
-    const uint64_t r1 = min(a.n, r0 + p.tr1);
-    constexpr int RA = sizeof(RowRaw<L, NA>) <= 80 ? 4 : 2;
-    RowRaw<L, NA> R[RA];
+    constexpr int R = part_rows<KW, NV>();
+    constexpr uint32_t TRA = PTA * R;
+    extern __shared__ uint32_t hs[];   // NB final-bucket counts, then F1 tile counts
+    const uint32_t NB = 1u << p.lb, F1 = 1u << p.f1;
+    uint32_t *h1 = hs + NB;
+    for (uint32_t i = threadIdx.x; i < NB; i += PTA) hs[i] = 0;
+    for (uint32_t t = blockIdx.x; t < p.tiles_a; t += gridDim.x) {
+        if (threadIdx.x < F1) h1[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t r0 = (uint64_t)t * TRA;
+        PRow<L, NV> R_[R];
 #pragma unroll
-    for (int u = 0; u < RA; ++u)
-        if (r0 + u * PTS + threadIdx.x < r1) issue_row<L, NA>(a, r0 + u * PTS + threadIdx.x, R[u]);
-    for (uint64_t r = r0; r < r1; r += RA * PTS) {
+        for (int u = 0; u < R; ++u) {
+            const uint64_t row = r0 + u * PTA + threadIdx.x;
+            prow_issue<L, NV, false>(a, p, row < a.n ? row : a.n - 1, R_[u]);
+        }
 #pragma unroll
-        for (int u = 0; u < RA; ++u) {
-            const uint64_t row = r + u * PTS + threadIdx.x;
-            uint32_t k[KW];
-            uint64_t rv[NA], rc[NA];
-            const bool ok = row < r1 && row_raw<L, NA>(a, row, R[u], k, rv, rc);
-            const uint64_t idx = a.fidx && row < r1 ? a.fidx[row] : row;
-            if (row + RA * PTS < r1) issue_row<L, NA>(a, row + RA * PTS, R[u]);
-            // this wave's kept rows take consecutive staging slots
-            const uint64_t m = __ballot(ok);
-            const uint32_t lane = threadIdx.x & 63, lead = m ? (uint32_t)__ffsll((long long)m) - 1 : 0;
-            uint32_t base = 0;
-            if (m && lane == lead) base = atomicAdd(&cnt_s, (uint32_t)__popcll(m));
-            base = __shfl(base, (int)lead);
-            if (ok) {
-                const uint32_t slot = base + (uint32_t)__popcll(m & lanemask_lt());
-                const uint32_t bk = hash_bits(hash_key<KW>(k), 0, p.f1);
-                uint32_t w[W];
-                rec_pack<KW, NA>(p, k, rv, rc, idx, w);
-#pragma unroll
-                for (int q = 0; q < W / 4; ++q)
-                    if ((uint32_t)q < p.rq)
-                        T.stage[slot * p.rq + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-                T.bkt[slot] = (uint16_t)bk;
-                atomicAdd(&T.hist[bk], 1u);
+        for (int u = 0; u < R; ++u) {
+            const uint64_t row = r0 + u * PTA + threadIdx.x;
+            if (row < a.n && prow_ok<L, NV>(a, row, R_[u])) {
+                const uint64_t h = hash_key<KW>(R_[u].k);
+                atomicAdd(&hs[hash_bits(h, 0, p.lb)], 1u);
+                atomicAdd(&h1[hash_bits(h, 0, p.f1)], 1u);
             }
         }
+        __syncthreads();
+        if (threadIdx.x < F1) p.cnt1[(uint64_t)t * F1 + threadIdx.x] = h1[threadIdx.x];
     }
     __syncthreads();
-    if (p.dbg & 1u) return;
-    tile_sort_write(T, cnt_s, F, p.rq, reinterpret_cast<uint4 *>(p.recs1) + (uint64_t)blockIdx.x * p.tr1 * p.rq,
-                    p.h1 + (uint64_t)blockIdx.x * (F + 1));
+    for (uint32_t i = threadIdx.x; i < NB; i += PTA)
+        if (hs[i]) atomicAdd(&p.hist[i], hs[i]);
 }
 
-// S1: per b1 (one block each), the exclusive prefix of its counts over the A tiles
-__global__ __launch_bounds__(1024) void k_gbp_colscan(PartArgs p) {
-    __shared__ uint32_t wsum[17];
-    const uint32_t b1 = blockIdx.x, F = 1u << p.f1;
-    const uint32_t per = (p.tiles1 + 1023) / 1024, t0 = threadIdx.x * per;
+// exclusive prefix (from r) of n values at stride `stride`, in place; loads go out 16 at a
+// time (a load-store-load chain on one array is one memory round trip per element)
+__device__ __forceinline__ void scan_column(uint32_t *v, uint32_t stride, uint32_t n, uint32_t r) {
+    for (uint32_t c0 = 0; c0 < n; c0 += 16) {
+        uint32_t x[16];
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) x[i] = c0 + i < n ? v[(uint64_t)(c0 + i) * stride] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+            if (c0 + i < n) v[(uint64_t)(c0 + i) * stride] = r;
+            r += x[i];
+        }
+    }
+}
+
+// O1: per chunk of CHT A tiles, rows per first-level bucket
+__global__ __launch_bounds__(PTA) void k_gbp_csum(PartArgs p) {
+    const uint32_t F1 = 1u << p.f1, c = blockIdx.x;
+    if (threadIdx.x >= F1) return;
+    const uint32_t t0 = c * CHT, t1 = min(p.tiles_a, t0 + CHT);
     uint32_t s = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t t = t0 + i;
-        if (t < p.tiles1) {
-            const uint32_t *h = p.h1 + (uint64_t)t * (F + 1);
-            s += h[b1 + 1] - h[b1];
-        }
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, wsum, total);
-    uint32_t *out = p.p1 + (uint64_t)b1 * (p.tiles1 + 1);
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t t = t0 + i;
-        if (t < p.tiles1) {
-            const uint32_t *h = p.h1 + (uint64_t)t * (F + 1);
-            out[t] = run;
-            run += h[b1 + 1] - h[b1];
-        }
-    }
-    if (threadIdx.x == 0) out[p.tiles1] = total;
+    for (uint32_t t = t0; t < t1; ++t) s += p.cnt1[(uint64_t)t * F1 + threadIdx.x];
+    p.csum[(uint64_t)c * F1 + threadIdx.x] = s;
 }
 
-// S2: b1's start in recs2 and its first B tile (one block)
-__global__ __launch_bounds__(1024) void k_gbp_base(PartArgs p) {
-    __shared__ uint32_t wsum[17];
-    const uint32_t F = 1u << p.f1;
-    const uint32_t per = (F + 1023) / 1024, b0 = threadIdx.x * per;
-    uint32_t s = 0, s2 = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t b = b0 + i;
-        if (b < F) {
-            const uint32_t c = p.p1[(uint64_t)b * (p.tiles1 + 1) + p.tiles1];
-            s += c;
-            s2 += (c + p.tr2 - 1) / p.tr2;
-        }
-    }
-    uint32_t total, total2;
-    uint32_t run = block_excl_scan(s, wsum, total);
-    uint32_t run2 = block_excl_scan(s2, wsum, total2);
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t b = b0 + i;
-        if (b < F) {
-            const uint32_t c = p.p1[(uint64_t)b * (p.tiles1 + 1) + p.tiles1];
-            p.base1[b] = run;
-            p.t2base[b] = run2;
-            run += c;
-            run2 += (c + p.tr2 - 1) / p.tr2;
-        }
-    }
-    if (threadIdx.x == 0) {
-        p.base1[F] = total;
-        p.t2base[F] = total2;
-    }
-}
-
-// the first index i in [lo, hi) with v[i] > x (v non-decreasing), by binary search
+// ---- S: bucket starts, cursors, chunk offsets, B tiles, C work items (one block) -----------
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t *v, uint32_t lo, uint32_t hi, uint32_t x) {
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -344,164 +286,189 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t *v, uint32_t 
     return lo;
 }
 
-// Flat positions over a list of segments (seg_pos: nseg + 1 prefix, in LDS).  The segment
-// holding the first position of each 64-position chunk of a round is found by binary search
-// (one per chunk, into cs[]); a lane then walks forward from its chunk's segment, a step or
-// two since segments hold tens of records.
-__device__ __forceinline__ void seg_chunk_starts(const uint32_t *seg_pos, uint32_t nseg, uint32_t q0, uint32_t end,
-                                                 uint32_t nchunk, uint32_t *cs) {
-    for (uint32_t c = threadIdx.x; c < nchunk; c += blockDim.x) {
-        const uint32_t q = q0 + 64 * c;
-        cs[c] = q < end ? upper_bound_u32(seg_pos, 0, nseg + 1, q) - 1 : 0u;
+__global__ __launch_bounds__(1024) void k_gbp_scan(PartArgs p) {
+    __shared__ uint32_t wsum[17];
+    __shared__ uint32_t ts[PART_F_MAX + 1];
+    const uint32_t NB = 1u << p.lb, F1 = 1u << p.f1, F2 = 1u << p.f2;
+    const uint32_t per = (NB + 1023) / 1024, b0 = threadIdx.x * per;
+    uint32_t s = 0, si = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t b = b0 + i;
+        const uint32_t c = b < NB ? p.hist[b] : 0u;
+        s += c;
+        si += (c + p.ch - 1) / p.ch;
     }
-}
-__device__ __forceinline__ uint32_t seg_of(const uint32_t *seg_pos, const uint32_t *cs, uint32_t q0, uint32_t q) {
-    uint32_t s = cs[(q - q0) >> 6];
-    while (seg_pos[s + 1] <= q) ++s;
-    return s;
-}
-
-// B tiles' b1 and the range of A tiles holding their records (the binary searches, done here
-// by one thread per B tile, would otherwise be dependent HBM round trips at each B block's start)
-__global__ __launch_bounds__(256) void k_gbp_bmap(PartArgs p) {
-    const uint32_t F1 = 1u << p.f1;
-    const uint32_t tile = blockIdx.x * 256 + threadIdx.x;
-    if (tile >= p.t2base[F1]) return;
-    const uint32_t b1 = upper_bound_u32(p.t2base, 0, F1 + 1, tile) - 1;
-    const uint32_t j = tile - p.t2base[b1];
-    const uint32_t *pb = p.p1 + (uint64_t)b1 * (p.tiles1 + 1);
-    const uint32_t q0 = j * p.tr2, q1 = min(pb[p.tiles1], q0 + p.tr2);
-    const uint32_t t0 = upper_bound_u32(pb, 0, p.tiles1 + 1, q0) - 1;
-    p.bmap[3 * tile] = b1;
-    p.bmap[3 * tile + 1] = t0;
-    p.bmap[3 * tile + 2] = upper_bound_u32(pb, t0, p.tiles1 + 1, q1 - 1) - 1;
-}
-
-// B: B tile `blockIdx.x` = records [j * tr2, (j + 1) * tr2) of its b1 (in A-tile order),
-// gathered from b1's segments of the A tiles, sorted by the next f2 bits
-template <int KW, int NA>
-__global__ __launch_bounds__(PTS) void k_gbp_b(PartArgs p) {
-    constexpr int W = PartRec<KW, NA>::W;
-    constexpr int U = 4;
-    extern __shared__ uint8_t lds_raw[];
-    const uint32_t F1 = 1u << p.f1, F2 = 1u << p.f2;
-    const uint32_t tile = blockIdx.x;
-    if (tile >= p.t2base[F1]) return;
-    const uint32_t b1 = p.bmap[3 * tile];
-    const uint32_t j = tile - p.t2base[b1];
-    const uint32_t *pb = p.p1 + (uint64_t)b1 * (p.tiles1 + 1);
-    const uint32_t q0 = j * p.tr2, q1 = min(pb[p.tiles1], q0 + p.tr2), cnt = q1 - q0;
-    const TileLds T = tile_lds(lds_raw, p.tr2, p.rq, F2);
-    uint32_t *seg_pos = T.wsum + 17;           // PSEGB + 1: prefix (in b1 order) of each mapped A tile
-    uint32_t *seg_src = seg_pos + PSEGB + 1;   // PSEGB: recs1 index of the segment's first record
-    uint32_t *cs = seg_src + PSEGB;            // tr2 / 64: segment of each 64-record chunk
-    for (uint32_t b = threadIdx.x; b < F2; b += PTS) T.hist[b] = 0;
-    uint32_t t = p.bmap[3 * tile + 1];
-    const uint32_t tl = p.bmap[3 * tile + 2];
-    for (uint32_t done = q0; done < q1;) {
-        __syncthreads();
-        const uint32_t nt = min(PSEGB, tl + 1 - t);
-        for (uint32_t i = threadIdx.x; i < nt; i += PTS) {
-            const uint32_t tt = t + i;
-            seg_pos[i] = pb[tt];
-            seg_src[i] = tt * p.tr1 + p.h1[(uint64_t)tt * (F1 + 1) + b1];
-        }
-        if (threadIdx.x == 0) seg_pos[nt] = pb[t + nt];
-        __syncthreads();
-        const uint32_t end = min(q1, seg_pos[nt]);
-        seg_chunk_starts(seg_pos, nt, done, end, (end - done + 63) / 64, cs);
-        __syncthreads();
-        // records [done, end): flat positions, U loads in flight per thread
-        for (uint32_t base = done; base < end && !(p.dbg & 2u); base += PTS * U) {
-            uint32_t w[U][W];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t q = base + (uint32_t)u * PTS + threadIdx.x;
-                if (q < end) {
-                    const uint32_t sg = seg_of(seg_pos, cs, done, q);
-                    recs_load<W>(p.recs1, (uint64_t)seg_src[sg] + (q - seg_pos[sg]), p.rq, w[u]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t q = base + (uint32_t)u * PTS + threadIdx.x;
-                if (q >= end) continue;
-                uint32_t k[KW];
-#pragma unroll
-                for (int i = 0; i < KW; ++i) k[i] = w[u][i];
-                const uint32_t b2 = hash_bits(hash_key<KW>(k), p.f1, p.f2);
-                const uint32_t slot = q - q0;
-#pragma unroll
-                for (int x = 0; x < W / 4; ++x)
-                    if ((uint32_t)x < p.rq)
-                        T.stage[slot * p.rq + x] = make_uint4(w[u][4 * x], w[u][4 * x + 1], w[u][4 * x + 2], w[u][4 * x + 3]);
-                T.bkt[slot] = (uint16_t)b2;
-                atomicAdd(&T.hist[b2], 1u);
-            }
-        }
-        done = end;
-        t += nt;
+    uint32_t tot, toti;
+    uint32_t run = block_excl_scan(s, wsum, tot);
+    uint32_t runi = block_excl_scan(si, wsum, toti);
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t b = b0 + i;
+        if (b >= NB) break;
+        const uint32_t c = p.hist[b], ni = (c + p.ch - 1) / p.ch;
+        p.start2[b] = run;
+        p.cur2[b] = run;
+        p.istart[b] = runi;
+        for (uint32_t k = 0; k < ni; ++k) p.itfb[runi + k] = b;
+        run += c;
+        runi += ni;
+    }
+    // first-level buckets: record counts, starts (= start2 of their first final bucket),
+    // chunk offsets and B tiles
+    uint32_t c1 = 0;
+    if (threadIdx.x < F1)
+        for (uint32_t b2 = 0; b2 < F2; ++b2) c1 += p.hist[threadIdx.x * F2 + b2];
+    uint32_t tot1, tott;
+    const uint32_t st1 = block_excl_scan(c1, wsum, tot1);
+    const uint32_t nt = (c1 + p.trb - 1) / p.trb;
+    const uint32_t tst = block_excl_scan(nt, wsum, tott);
+    if (threadIdx.x < F1) {
+        scan_column(p.csum + threadIdx.x, F1, p.nchunk, st1);
+        p.tstart[threadIdx.x] = tst;
+        ts[threadIdx.x] = tst;
+    }
+    if (threadIdx.x == 0) {
+        p.start2[NB] = tot;
+        p.istart[NB] = toti;
+        p.tstart[F1] = tott;
+        ts[F1] = tott;
+        p.ctl[0] = 0;
+        p.ctl[1] = tott;
+        p.ctl[2] = toti;
     }
     __syncthreads();
-    if (p.dbg & 4u) return;
-    tile_sort_write(T, cnt, F2, p.rq,
-                    reinterpret_cast<uint4 *>(p.recs2) + ((uint64_t)p.base1[b1] + q0) * p.rq,
-                    p.h2 + (uint64_t)tile * (F2 + 1));
+    for (uint32_t t = threadIdx.x; t < tott; t += 1024) p.bt[t] = upper_bound_u32(ts, 0, F1 + 1, t) - 1;
 }
 
-// I: aggregate work items per final bucket (a block per b1, a thread per b2), then their
-// prefix (one block)
-__global__ __launch_bounds__(256) void k_gbp_icount(PartArgs p) {
-    const uint32_t F2 = 1u << p.f2;
-    const uint32_t b1 = blockIdx.x;
-    const uint32_t j0 = p.t2base[b1], j1 = p.t2base[b1 + 1];
-    for (uint32_t b2 = threadIdx.x; b2 < F2; b2 += 256) {
-        uint32_t n = 0;
-        uint32_t j = j0;
-        for (; j + 8 <= j1; j += 8) {   // eight independent loads per step
-            uint32_t c[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t *h = p.h2 + (uint64_t)(j + u) * (F2 + 1);
-                c[u] = h[b2 + 1] - h[b2];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) n += c[u];
-        }
-        for (; j < j1; ++j) {
-            const uint32_t *h = p.h2 + (uint64_t)j * (F2 + 1);
-            n += h[b2 + 1] - h[b2];
-        }
-        // a chunk of at most ch records and at most PSEG B tiles per item
-        p.items[(b1 << p.f2) | b2] = n ? max((n + p.ch - 1) / p.ch, (j1 - j0 + PSEG - 1) / PSEG) : 0u;
+// O2: each A tile's exact output position per first-level bucket (cnt1 in place)
+__global__ __launch_bounds__(PTA) void k_gbp_offs(PartArgs p) {
+    const uint32_t F1 = 1u << p.f1, c = blockIdx.x;
+    if (threadIdx.x >= F1) return;
+    const uint32_t t0 = c * CHT, t1 = min(p.tiles_a, t0 + CHT);
+    scan_column(p.cnt1 + (uint64_t)t0 * F1 + threadIdx.x, F1, t1 - t0, p.csum[(uint64_t)c * F1 + threadIdx.x]);
+}
+
+// ---- A: a tile of rows -> records, each first-level bucket's run at its exact position -----
+// The tile's rows stay in registers (R per thread, all loads issued at once); a row's rank
+// in its bucket comes from an LDS atomic, so the records are staged in LDS already sorted
+// and leave as whole runs, 16 B per lane.
+template <class L, int NV>
+__global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
+    constexpr int KW = L::KW;
+    constexpr int R = part_rows<KW, NV>();
+    constexpr uint32_t TRA = PTA * R;
+    extern __shared__ uint8_t lds_raw[];
+    const uint32_t F = 1u << p.f1, rq = p.rq;
+    uint4 *stage = reinterpret_cast<uint4 *>(lds_raw);                   // TRA x rq quads, sorted
+    uint8_t *sb = lds_raw + (size_t)TRA * rq * 16;                       // TRA: bucket of each position
+    uint32_t *hist = reinterpret_cast<uint32_t *>(sb + TRA);             // F
+    uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
+    const uint32_t t = blockIdx.x;
+    if (threadIdx.x < F) {
+        hist[threadIdx.x] = 0;
+        base[threadIdx.x] = p.cnt1[(uint64_t)t * F + threadIdx.x];
     }
-}
-
-__global__ __launch_bounds__(1024) void k_gbp_iscan(PartArgs p) {
-    __shared__ uint32_t wsum[17];
-    const uint32_t nb = 1u << (p.f1 + p.f2);
-    const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < per; ++i) s += b0 + i < nb ? p.items[b0 + i] : 0u;
+    __syncthreads();
+    const uint64_t r0 = (uint64_t)t * TRA;
+    PRow<L, NV> R_[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint64_t row = r0 + u * PTA + threadIdx.x;
+        prow_issue<L, NV, true>(a, p, row < a.n ? row : a.n - 1, R_[u]);
+    }
+    uint32_t bk[R], rk[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const uint64_t row = r0 + u * PTA + threadIdx.x;
+        bk[u] = 0xFFFFFFFFu;
+        if (row < a.n && prow_ok<L, NV>(a, row, R_[u])) {
+            bk[u] = hash_bits(hash_key<KW>(R_[u].k), 0, p.f1);
+            rk[u] = atomicAdd(&hist[bk[u]], 1u);
+        }
+    }
+    __syncthreads();
     uint32_t total;
-    uint32_t run = block_excl_scan(s, wsum, total);
-    for (uint32_t i = 0; i < per; ++i) {
-        if (b0 + i < nb) {
-            const uint32_t c = p.items[b0 + i];
-            p.items[b0 + i] = run;
-            run += c;
-        }
+    const uint32_t o = block_excl_scan(threadIdx.x < F ? hist[threadIdx.x] : 0u, wsum, total);
+    if (threadIdx.x < F) off[threadIdx.x] = o;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        if (bk[u] == 0xFFFFFFFFu) continue;
+        const uint64_t row = r0 + u * PTA + threadIdx.x;
+        const uint32_t pos = off[bk[u]] + rk[u];
+        prow_stage<L, NV>(p, row, R_[u], reinterpret_cast<uint32_t *>(stage + pos * rq));
+        sb[pos] = (uint8_t)bk[u];
     }
-    if (threadIdx.x == 0) p.items[nb] = total;
+    __syncthreads();
+    if (p.dbg & 1u) return;
+    uint4 *out = reinterpret_cast<uint4 *>(p.recs1);
+    const uint32_t nq = total * rq;
+    for (uint32_t qi = threadIdx.x; qi < nq; qi += PTA) {
+        const uint32_t j = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
+        const uint32_t q = qi - j * rq, b = sb[j];
+        out[(uint64_t)(base[b] + j - off[b]) * rq + q] = stage[qi];
+    }
 }
 
-// aggregate work item -> its final bucket (one thread per item; the C blocks would otherwise
-// start every item with a dependent binary search in HBM)
-__global__ __launch_bounds__(256) void k_gbp_imap(PartArgs p) {
-    const uint32_t nb = 1u << (p.f1 + p.f2);
-    const uint32_t n = min(p.items[nb], p.imax);
-    for (uint32_t it = blockIdx.x * 256 + threadIdx.x; it < n; it += gridDim.x * 256)
-        p.imap[it] = upper_bound_u32(p.items, 0, nb + 1, it) - 1;
+// ---- B: a tile of one first-level bucket's records -> its final buckets --------------------
+// B tile `blockIdx.x` = records [j * trb, (j + 1) * trb) of first-level bucket b1 in recs1
+// (contiguous): loaded flat into LDS (coalesced), ranked by the next f2 hash bits with LDS
+// atomics, and each final bucket's run written at a cursor reserved with one atomic.
+template <int KW, int NV>
+__global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
+    constexpr int U = 16;              // quads in flight per thread: a whole tile at once
+    extern __shared__ uint8_t lds_raw[];
+    const uint32_t tile = blockIdx.x;
+    if (tile >= p.ctl[1]) return;
+    const uint32_t F = 1u << p.f2, rq = p.rq, trb = p.trb;
+    uint4 *stage = reinterpret_cast<uint4 *>(lds_raw);                   // trb x rq quads, input order
+    uint16_t *bkt = reinterpret_cast<uint16_t *>(lds_raw + (size_t)trb * rq * 16);
+    uint16_t *rank = bkt + trb, *perm = rank + trb;
+    uint32_t *hist = reinterpret_cast<uint32_t *>(perm + trb);
+    uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
+    const uint32_t b1 = p.bt[tile];
+    const uint32_t j = tile - p.tstart[b1];
+    const uint32_t s = p.start2[b1 << p.f2] + j * trb;
+    const uint32_t e = min(p.start2[(b1 + 1) << p.f2], s + trb);
+    const uint32_t cnt = e - s;
+    if (threadIdx.x < F) hist[threadIdx.x] = 0;
+    const u4v *src = reinterpret_cast<const u4v *>(p.recs1) + (uint64_t)s * rq;
+    const uint32_t nq = cnt * rq;
+    for (uint32_t q0 = threadIdx.x; q0 < nq && !(p.dbg & 2u); q0 += PTA * U) {
+        u4v x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q0 + u * PTA < nq) x[u] = __builtin_nontemporal_load(src + q0 + u * PTA);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q0 + u * PTA < nq) stage[q0 + u * PTA] = make_uint4(x[u].x, x[u].y, x[u].z, x[u].w);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += PTA) {
+        uint32_t k[KW];
+        lds_key<KW>(p, reinterpret_cast<const uint32_t *>(stage + i * rq), k);
+        const uint32_t b2 = hash_bits(hash_key<KW>(k), p.f1, p.f2);
+        bkt[i] = (uint16_t)b2;
+        rank[i] = (uint16_t)atomicAdd(&hist[b2], 1u);
+    }
+    __syncthreads();
+    const uint32_t c = threadIdx.x < F ? hist[threadIdx.x] : 0u;
+    uint32_t total;
+    const uint32_t o = block_excl_scan(c, wsum, total);
+    if (threadIdx.x < F) {
+        off[threadIdx.x] = o;
+        base[threadIdx.x] = c ? atomicAdd(p.cur2 + (b1 << p.f2) + threadIdx.x, c) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += PTA) perm[off[bkt[i]] + rank[i]] = (uint16_t)i;
+    __syncthreads();
+    if (p.dbg & 4u) return;
+    uint4 *out = reinterpret_cast<uint4 *>(p.recs2);
+    for (uint32_t qi = threadIdx.x; qi < nq; qi += PTA) {
+        const uint32_t jj = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
+        const uint32_t q = qi - jj * rq;
+        const uint32_t sidx = perm[jj], b = bkt[sidx];
+        out[(uint64_t)(base[b] + jj - off[b]) * rq + q] = stage[sidx * rq + q];
+    }
 }
 
 // ---- C: an LDS hash table per work item ----------------------------------------------------
@@ -509,50 +476,86 @@ template <int KW>
 struct AggTab {
     uint64_t *first;     // E: min event index (~0 = none yet)
     uint64_t *agg;       // naggs x E
-    uint32_t *tag;       // E: 0 = empty, else the hash's low word | 1 (set once, by the claimer)
-    uint32_t *st;        // E: 1 once the claimer has written the key
+    uint32_t *tag;       // E: 0 = empty, TAG_BUSY = claimed, key being written, else the hash's low
+                         // word | 1 (odd: published, the key words are valid)
     uint32_t *key;       // E x KW
     uint32_t *occ_old;   // occw: the bucket's occupancy bitmap words before this flush
     uint32_t *occ_new;   // occw: slots claimed by this flush
-    uint32_t *seg_pos;   // PSEG + 1: prefix of the item's segments
-    uint32_t *seg_src;   // PSEG: recs2 index of each segment's first record
-    uint32_t *cs;        // PT / 64: segment of each 64-record chunk of a round
-    uint32_t *flag;      // [0] some row of the item took the HBM path
+    uint32_t *flag;      // [0] some row of the item took the HBM path, [1] the item
     uint32_t E;
 };
+constexpr uint32_t TAG_BUSY = 2;
 
-// find or insert the key's entry; -1 when maxp entries were probed without a match or a free
-// one (the row then goes to HBM).  A lane that finds its key's entry claimed but not yet
-// published looks again on the next pass of the loop instead of spinning in place, so a
-// claimer in the same wave (whose key stores follow the CAS in program order) always gets
-// to publish first.
+__host__ __device__ constexpr size_t agg_entry_bytes(uint32_t kw, uint32_t naggs) { return 12 + 4 * (size_t)kw + 8 * (size_t)naggs; }
+
+// every key word of entry e compared with k: all loads issued before any compare (a
+// short-circuit compare is one dependent LDS round trip per word)
+template <int KW>
+__device__ __forceinline__ bool at_key_eq(const AggTab<KW> &T, uint32_t e, const uint32_t (&k)[KW]) {
+    const uint32_t *p = T.key + (uint64_t)e * KW;
+    uint32_t d[KW];
+    if constexpr (KW % 4 == 0) {
+#pragma unroll
+        for (int w = 0; w < KW; w += 4) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(p + w);
+            d[w] = q.x; d[w + 1] = q.y; d[w + 2] = q.z; d[w + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < KW; ++w) d[w] = p[w];
+    }
+    uint32_t diff = 0;
+#pragma unroll
+    for (int w = 0; w < KW; ++w) diff |= d[w] ^ k[w];
+    return diff == 0;
+}
+
+// find or insert the key's entry; -1 when maxp sets were probed without a match or a free
+// entry (the row then goes to HBM).  The table is 8-way set associative on the hash's low
+// word: one lookup reads a set's 8 tags with two 16-B LDS loads and compares full keys only
+// on a tag match, so a wave resolves nearly every row in one step (a linear probe makes the
+// whole wave iterate as long as its longest chain).  A claimer CASes an empty tag 0 ->
+// TAG_BUSY, writes the key, then stores the odd tag; a lane that meets TAG_BUSY in its set
+// reads the set again (the claimer is between two LDS stores).
 template <int KW>
 __device__ __forceinline__ int at_find_insert(const AggTab<KW> &T, const uint32_t (&k)[KW], uint64_t h, uint32_t maxp) {
-    const uint32_t t = (uint32_t)h | 1u;
-    uint32_t e = (uint32_t)(((uint64_t)(uint32_t)h * T.E) >> 32);
+    const uint32_t t = (uint32_t)h | 1u, nsets = T.E >> 3;
+    uint32_t set = (uint32_t)(((uint64_t)(uint32_t)h * nsets) >> 32);
     for (uint32_t probes = 0, looks = 0;;) {
-        uint32_t cur = __hip_atomic_load(&T.tag[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == 0) {
-            cur = atomicCAS(&T.tag[e], 0u, t);
-            if (cur == 0) {
+        const uint32_t base = set * 8;
+        asm volatile("" ::: "memory");   // the set is read afresh on every pass
+        const uint4 t0 = *reinterpret_cast<const uint4 *>(T.tag + base);
+        const uint4 t1 = *reinterpret_cast<const uint4 *>(T.tag + base + 4);
+        const uint32_t tg[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+        uint32_t mt = 0, mb = 0, me = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            mt |= (tg[j] == t ? 1u : 0u) << j;
+            mb |= (tg[j] == TAG_BUSY ? 1u : 0u) << j;
+            me |= (tg[j] == 0 ? 1u : 0u) << j;
+        }
+        if (mt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        while (mt) {   // usually one candidate
+            const uint32_t e = base + (uint32_t)(__builtin_ffs((int)mt) - 1);
+            mt &= mt - 1;
+            if (at_key_eq<KW>(T, e, k)) return (int)e;
+        }
+        if (mb) {   // a claim in progress in this set: it may be this key
+            if (++looks > SPIN_LIMIT) return -1;   // never expected; the HBM path stays exact
+            continue;
+        }
+        if (me) {
+            const uint32_t e = base + (uint32_t)(__builtin_ffs((int)me) - 1);
+            if (atomicCAS(&T.tag[e], 0u, TAG_BUSY) == 0u) {
 #pragma unroll
                 for (int w = 0; w < KW; ++w) T.key[(uint64_t)e * KW + w] = k[w];
-                __hip_atomic_store(&T.st[e], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&T.tag[e], t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 return (int)e;
             }
+            continue;   // lost the entry: read the set again
         }
-        if (cur == t) {
-            if (__hip_atomic_load(&T.st[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
-                if (++looks > SPIN_LIMIT) return -1;   // never expected; the HBM path stays exact
-                continue;
-            }
-            bool eq = true;
-#pragma unroll
-            for (int w = 0; w < KW; ++w) eq = eq && T.key[(uint64_t)e * KW + w] == k[w];
-            if (eq) return (int)e;
-        }
-        if (++probes >= maxp) return -1;
-        e = e + 1 == T.E ? 0 : e + 1;
+        if (++probes >= maxp) return -1;   // set full
+        set = set + 1 == nsets ? 0 : set + 1;
     }
 }
 
@@ -574,9 +577,14 @@ __device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[K
 // an LDS group written to a final bucket this item owns alone: plain loads and stores
 template <int KW, int NA>
 __device__ __forceinline__ void flush_owned(const GbArgs &a, const AggTab<KW> &T, const uint32_t (&k)[KW],
-                                            uint64_t h, const uint64_t (&v)[NA], uint64_t f, uint64_t sb) {
+                                            uint64_t h, const uint64_t (&v)[NA], uint64_t f, uint64_t sb,
+                                            uint32_t p_sb_log) {
     constexpr uint32_t KOFF = koff_of(KW);
     uint64_t s = home_slot(a, h);
+    if ((s >> p_sb_log) != (sb >> p_sb_log)) {   // never expected: a record in the wrong bucket
+        atomicOr(a.err, 32u);
+        return;
+    }
     for (uint32_t probe = 0; probe < a.max_probe; ++probe, s = next_slot(a, s)) {
         const uint32_t l = (uint32_t)(s - sb), wd = l >> 5, bit = 1u << (l & 31);
         if (T.occ_new[wd] & bit) continue;   // claimed by another group of this flush
@@ -605,133 +613,171 @@ __device__ __forceinline__ void flush_owned(const GbArgs &a, const AggTab<KW> &T
     atomicOr(a.err, 4u);
 }
 
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// Wave64 pre-combine (a whole wave calls it): the lowest lane still to be merged leads; the
+// lanes holding the same key (hash, then every key word, compared with the leader's) hand
+// over their values -- sums and the first index reduced across the wave with shuffles -- and
+// drop their rows.  A round that finds no duplicate of its leader ends the pre-combine: on a
+// near-uniform stream it costs one round of hash shuffles per 64 rows; on a skewed bucket
+// the hot key's rows become one LDS update per wave instead of a queue of same-address
+// LDS atomics.
 template <int KW, int NA>
-__global__ __launch_bounds__(PT) void k_gbp_c(GbArgs a, PartArgs p) {
-    constexpr int W = PartRec<KW, NA>::W;
+__device__ __forceinline__ void wave_combine(const GbArgs &a, uint32_t rounds, bool &ok, const uint32_t (&k)[KW],
+                                             uint64_t h, uint64_t (&v)[NA], uint64_t &gidx) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t todo = __ballot(ok);
+    for (uint32_t r = 0; r < rounds && todo; ++r) {
+        const int L = __ffsll((long long)todo) - 1;
+        const uint64_t hl = __shfl((unsigned long long)h, L);
+        bool same = ((todo >> lane) & 1ull) && h == hl;
+        if (__popcll(__ballot(same)) < 2) break;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) {
+            const uint32_t kl = __shfl(k[w], L);
+            same = same && k[w] == kl;
+        }
+        const uint64_t peers = __ballot(same);
+        todo &= ~peers;
+        if (__popcll(peers) < 2) continue;
+#pragma unroll
+        for (int x = 0; x < NA; ++x) {
+            if (x < (int)a.naggs) {
+                const unsigned long long s = wave_sum_u64(same ? (unsigned long long)v[x] : 0ull);
+                if ((int)lane == L) v[x] = s;
+            }
+        }
+        const unsigned long long f = wave_min_u64(same ? (unsigned long long)gidx : ~0ull);
+        if ((int)lane == L) gidx = f;
+        else if (same) ok = false;
+    }
+}
+
+// C: work items from a dequeue; per item an LDS hash table, then the groups into HBM.
+// An item's records are contiguous: they are read in rounds of UC x PTC records as flat
+// 16-B quads (the next round's quads in registers while this round is aggregated from LDS).
+constexpr uint32_t UCMAX = 2;
+
+template <int KW>
+__device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<KW> &T, bool ok,
+                                      const uint32_t *rec) {
+    uint32_t k[KW];
+    uint64_t v[AMAX], gidx = 0;
+    lds_decode<KW>(a, p, rec, k, v, gidx);
+    const uint64_t hh = hash_key<KW>(k);
+    if (p.combine) wave_combine<KW, AMAX>(a, p.combine, ok, k, hh, v, gidx);   // IGX_GBP_COMBINE
+    if (!ok || (p.dbg & 32u)) return;
+    const int ei = at_find_insert<KW>(T, k, hh, p.maxp);
+    if (p.dbg & 64u) return;   // diagnostics: no accumulation
+    if (ei >= 0) {
+#pragma unroll
+        for (int x = 0; x < AMAX; ++x)
+            if (x < (int)a.naggs && v[x])
+                atomicAdd(reinterpret_cast<unsigned long long *>(&T.agg[(uint64_t)x * T.E + ei]), (unsigned long long)v[x]);
+        atomicMin(reinterpret_cast<unsigned long long *>(&T.first[ei]), (unsigned long long)gidx);
+    } else {
+        T.flag[0] = 1;
+        hbm_merge<KW, AMAX>(a, k, hh, v, gidx);
+    }
+}
+
+template <int KW, int NV>
+__global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
+    constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
+    constexpr int NA = AMAX;
     extern __shared__ uint64_t lds[];
     AggTab<KW> T;
-    const uint32_t E = p.E;
+    const uint32_t E = p.E, rq = p.rq, uc = p.uc, RC = uc * PTC;
     T.E = E;
     T.first = lds;
     T.agg = lds + E;
     T.tag = reinterpret_cast<uint32_t *>(lds + (uint64_t)(1 + a.naggs) * E);
-    T.st = T.tag + E;
-    T.key = T.st + E;
+    T.key = T.tag + E;
     T.occ_old = T.key + (uint64_t)E * KW;
     T.occ_new = T.occ_old + p.occw;
-    T.seg_pos = T.occ_new + p.occw;
-    T.seg_src = T.seg_pos + PSEG + 1;
-    T.cs = T.seg_src + PSEG;
-    T.flag = T.cs + PT / 64;
-    const uint32_t F2 = 1u << p.f2, nb = 1u << (p.f1 + p.f2);
-    const uint32_t nitems = min(p.items[nb], p.imax);
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const uint32_t fb = p.imap[it];   // items[fb] <= it < items[fb + 1]
-        const uint32_t nit = p.items[fb + 1] - p.items[fb], kx = it - p.items[fb];
-        const uint32_t b1 = fb >> p.f2, b2 = fb & (F2 - 1);
-        const uint32_t J = p.t2base[b1 + 1] - p.t2base[b1];
-        const uint32_t j0 = p.t2base[b1] + (uint32_t)((uint64_t)J * kx / nit);
-        const uint32_t j1 = p.t2base[b1] + (uint32_t)((uint64_t)J * (kx + 1) / nit);
-        const uint32_t nseg = j1 - j0;   // <= PSEG (k_gbp_icount)
-        for (uint32_t e = threadIdx.x; e < E; e += PT) {
-            T.tag[e] = 0;
-            T.st[e] = 0;
-            T.first[e] = ~0ull;
-            for (uint32_t x = 0; x < a.naggs; ++x) T.agg[(uint64_t)x * E + e] = 0;
+    T.flag = T.occ_new + p.occw;
+    uint4 *stage = reinterpret_cast<uint4 *>(T.flag + 4);   // RC x rq quads (16-B aligned: see the launch)
+    const u4v *recs = reinterpret_cast<const u4v *>(p.recs2);
+    const uint32_t nitems = p.ctl[2];
+    for (;;) {
+        if (threadIdx.x == 0) T.flag[1] = atomicAdd(&p.ctl[0], 1u);
+        for (uint32_t x = threadIdx.x; x < E; x += PTC) {
+            T.tag[x] = 0;
+            T.first[x] = ~0ull;
+            for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
         }
-        if (threadIdx.x == 0) *T.flag = 0;
-        // the item's segments: bucket b2 of each B tile j in [j0, j1)
-        __shared__ uint32_t wsum[17];
-        uint32_t len = 0, src = 0;
-        if (threadIdx.x < nseg) {
-            const uint32_t jj = j0 + threadIdx.x;
-            const uint32_t *h = p.h2 + (uint64_t)jj * (F2 + 1);
-            len = h[b2 + 1] - h[b2];
-            src = p.base1[b1] + (jj - p.t2base[b1]) * p.tr2 + h[b2];
-        }
-        uint32_t total;
-        const uint32_t off = block_excl_scan(len, wsum, total);
-        if (threadIdx.x < nseg) {
-            T.seg_pos[threadIdx.x] = off;
-            T.seg_src[threadIdx.x] = src;
-        }
-        if (threadIdx.x == 0) T.seg_pos[nseg] = total;
+        if (threadIdx.x == 0) T.flag[0] = 0;
         __syncthreads();
+        const uint32_t it = T.flag[1];
+        if (it >= nitems) break;
+        const uint32_t fb = p.itfb[it];
+        const uint32_t i0 = p.istart[fb], nit = p.istart[fb + 1] - i0, kx = it - i0;
+        const uint32_t s0 = p.start2[fb], len = p.start2[fb + 1] - s0;
+        const uint32_t s = s0 + (uint32_t)((uint64_t)len * kx / nit);
+        const uint32_t e = s0 + (uint32_t)((uint64_t)len * (kx + 1) / nit);
+        const uint64_t qlast = (uint64_t)e * rq - 1;   // the item's last quad (loads clamp to it)
 
-        // rounds of PT records; the next round's loads are issued before this one is processed
-        uint32_t w[2][W];
-        if (!(p.dbg & 8u) && total) {
-            seg_chunk_starts(T.seg_pos, nseg, 0, min(total, PT), (min(total, PT) + 63) / 64, T.cs);
+        u4v pf[UCMAX * QM];
+        const uint32_t mq = uc * rq;
+        auto prefetch = [&](uint32_t r0) {
+#pragma unroll
+            for (uint32_t m = 0; m < UCMAX * QM; ++m)
+                if (m < mq) pf[m] = __builtin_nontemporal_load(recs + min((uint64_t)r0 * rq + m * PTC + threadIdx.x, qlast));
+        };
+        if (s < e && !(p.dbg & 8u)) prefetch(s);
+        for (uint32_t r0 = s; r0 < e && !(p.dbg & 8u); r0 += RC) {
+            const uint32_t nq = min(RC, e - r0) * rq;
+            __syncthreads();   // the previous round's records are no longer read
+#pragma unroll
+            for (uint32_t m = 0; m < UCMAX * QM; ++m)
+                if (m < mq && m * PTC + threadIdx.x < nq)
+                    stage[m * PTC + threadIdx.x] = make_uint4(pf[m].x, pf[m].y, pf[m].z, pf[m].w);
             __syncthreads();
-            if (threadIdx.x < total) {
-                const uint32_t sg = seg_of(T.seg_pos, T.cs, 0, threadIdx.x);
-                recs_load<W>(p.recs2, (uint64_t)T.seg_src[sg] + (threadIdx.x - T.seg_pos[sg]), p.rq, w[0]);
-            }
-        }
-        for (uint32_t base = 0; base < total && !(p.dbg & 8u); base += 2 * PT) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t cur = base + h * PT, nxt = cur + PT;
-                if (cur >= total) break;
-                __syncthreads();   // every lane has read cs for the current round
-                if (nxt < total) seg_chunk_starts(T.seg_pos, nseg, nxt, min(total, nxt + PT), (min(total, nxt + PT) - nxt + 63) / 64, T.cs);
-                __syncthreads();
-                if (nxt + threadIdx.x < total) {
-                    const uint32_t q = nxt + threadIdx.x;
-                    const uint32_t sg = seg_of(T.seg_pos, T.cs, nxt, q);
-                    recs_load<W>(p.recs2, (uint64_t)T.seg_src[sg] + (q - T.seg_pos[sg]), p.rq, w[1 - h]);
-                }
-                if (cur + threadIdx.x >= total) continue;
-                uint32_t k[KW];
-                uint64_t v[NA], gidx;
-                rec_decode<KW, NA>(a, p, w[h], k, v, gidx);
-                const uint64_t hh = hash_key<KW>(k);
-                if (p.dbg & 32u) {   // diagnostics: records loaded and hashed only
-                    if (hh == 0x1234567ull && gidx == 7) *T.flag = 2;
-                    continue;
-                }
-                const int e = at_find_insert<KW>(T, k, hh, p.maxp);
-                if (p.dbg & 64u) continue;   // diagnostics: no accumulation
-                if (e >= 0) {
-#pragma unroll
-                    for (int x = 0; x < NA; ++x)
-                        if (x < (int)a.naggs && v[x])
-                            atomicAdd(reinterpret_cast<unsigned long long *>(&T.agg[(uint64_t)x * E + e]),
-                                      (unsigned long long)v[x]);
-                    atomicMin(reinterpret_cast<unsigned long long *>(&T.first[e]), (unsigned long long)gidx);
-                } else {
-                    *T.flag = 1;
-                    hbm_merge<KW, NA>(a, k, hh, v, gidx);
-                }
+            if (r0 + RC < e) prefetch(r0 + RC);
+            for (uint32_t u = 0; u < uc; ++u) {
+                const uint32_t i = u * PTC + threadIdx.x;
+                c_row<KW>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
             }
         }
         __syncthreads();
 
         // the item's groups into the HBM table
-        const bool owned = nit == 1 && *T.flag == 0;
+        const bool owned = nit == 1 && T.flag[0] == 0;
         const uint64_t sb = (uint64_t)fb << p.sb_log;
         if (owned) {
-            for (uint32_t i = threadIdx.x; i < p.occw; i += PT) {
+            for (uint32_t i = threadIdx.x; i < p.occw; i += PTC) {
                 T.occ_old[i] = a.occ[(sb >> 5) + i];
                 T.occ_new[i] = 0;
             }
             __syncthreads();
         }
-        for (uint32_t e = threadIdx.x; e < E && !(p.dbg & 16u); e += PT) {
-            if (!T.st[e]) continue;
+        for (uint32_t x = threadIdx.x; x < E && !(p.dbg & 16u); x += PTC) {
+            if (!T.tag[x]) continue;
             uint32_t k[KW];
 #pragma unroll
-            for (int x = 0; x < KW; ++x) k[x] = T.key[(uint64_t)e * KW + x];
+            for (int q = 0; q < KW; ++q) k[q] = T.key[(uint64_t)x * KW + q];
             uint64_t v[NA];
 #pragma unroll
-            for (int x = 0; x < NA; ++x) v[x] = x < (int)a.naggs ? T.agg[(uint64_t)x * E + e] : 0ull;
+            for (int q = 0; q < NA; ++q) v[q] = q < (int)a.naggs ? T.agg[(uint64_t)q * E + x] : 0ull;
             const uint64_t h = hash_key<KW>(k);
-            if (owned) flush_owned<KW, NA>(a, T, k, h, v, T.first[e], sb);
-            else hbm_merge<KW, NA>(a, k, h, v, T.first[e]);
+            if (owned) flush_owned<KW, NA>(a, T, k, h, v, T.first[x], sb, p.sb_log);
+            else hbm_merge<KW, NA>(a, k, h, v, T.first[x]);
         }
         __syncthreads();
         if (owned) {
-            for (uint32_t i = threadIdx.x; i < p.occw; i += PT)
+            for (uint32_t i = threadIdx.x; i < p.occw; i += PTC)
                 if (T.occ_new[i]) a.occ[(sb >> 5) + i] = T.occ_old[i] | T.occ_new[i];
             __syncthreads();
         }
