@@ -370,7 +370,9 @@ def run_c4(a, ctx):
                        + (", partial groups all-to-all by key owner + owner merge" if world > 1 else ""),
            "events_per_gpu": n, "value": world * n / (ms * 1e-3), "unit": "events/s", "ms_per_step": ms,
            "distinct_on_rank0": ng,
-           "roofline": roofline(n * 24 + st["G"] * 20, clk.avg(), "k_groupby<np tuple>",
+           "roofline": roofline(n * 24 + st["G"] * 20, clk.avg(),
+                                "igx_groupby_update on the np tuple (AUTO: the partitioned form's passes "
+                                "k_gbp_count/csum/scan/offs/a/b/c after the first, measured, interval)",
                                 "24 B/event (src 4, peer 4, port 2, pkt 1, type 1, proto 1, hostip 4, raddr 4, "
                                 "+3 pad) + 20 B/distinct tuple (key 12 + first 8)", "c4", {"events": n})}
     out["roofline"]["alg_bytes_per_launch"] = alg

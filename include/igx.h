@@ -303,9 +303,11 @@ int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete lo
  *                  streams, where nearly every row would miss the cache);
  *   IGX_GB_PART    rows are radix-partitioned by key hash in two streamed passes and each
  *                  final bucket is aggregated in LDS, then written to the table with plain
- *                  stores (no atomics; DESIGN.md §4 has its measured cost);
+ *                  stores (no atomics; DESIGN.md §4 has its measured cost).  Scratch: two
+ *                  record buffers of nrows x 16..128 B;
  *   IGX_GB_AUTO    (default) cached; an interval in which more than 90% of the rows missed
- *                  the cache switches the next 16 intervals to direct, then measures again.
+ *                  the cache switches the next 16 intervals to partitioned, then measures
+ *                  again.
  * The mode of an interval is fixed by its first update. */
 enum igx_gb_mode { IGX_GB_AUTO = 0, IGX_GB_CACHED = 1, IGX_GB_DIRECT = 2, IGX_GB_PART = 3 };
 int igx_groupby_set_mode(igx_table *t, uint32_t mode);

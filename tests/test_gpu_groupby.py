@@ -367,7 +367,7 @@ def test_direct_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layou
     """IGX_GB_DIRECT (no LDS cache: every row probes the HBM table, k_groupby_direct) gives
     the same table as the oracle -- keys, every aggregate (incl. a u32 wrap), first index --
     over three chunked updates with a running base index and a nil mask; then AUTO switches
-    a miss-heavy stream to the direct form after one measured interval and stays exact."""
+    a miss-heavy stream to the partitioned form after one measured interval and stays exact."""
     A = igx._abi
     n = 450_000
     rng = np.random.default_rng(4)
@@ -410,7 +410,7 @@ def test_direct_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layou
     for a, b in zip(cuts, cuts[1:]):
         tab.update([c[a:b] for c in cols], list(range(len(names))), b - a, 9 + a, valid=dv[a:b])
     _check(E, H, tab, widths, *o)
-    # AUTO: interval 1 runs cached and measures; a miss-heavy stream runs direct next
+    # AUTO: interval 1 runs cached and measures; a miss-heavy stream runs partitioned next
     tab.set_mode(A.GB_AUTO)
     for _ in range(3):
         tab.reset()

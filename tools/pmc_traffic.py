@@ -37,16 +37,24 @@ def main():
     p.add_argument("--fetch", required=True)
     p.add_argument("--write", required=True)
     p.add_argument("--kernel", default="k_groupby")
+    p.add_argument("--anchor", default=None,
+                   help="a chain of kernels per update (the partitioned form): sum every --kernel match "
+                        "and divide by the launches of this one")
     p.add_argument("--config", required=True)
     p.add_argument("--out", required=True)
     a = p.parse_args()
     f = _values(a.fetch, "FETCH_SIZE", a.kernel)
     w = _values(a.write, "WRITE_SIZE", a.kernel)
-    fetch_b = 2.0 * 1024.0 * sum(f) / len(f)
-    write_b = 1024.0 * sum(w) / len(w)
+    nf, nw = len(f), len(w)
+    if a.anchor:
+        nf = len(_values(a.fetch, "FETCH_SIZE", a.anchor))
+        nw = len(_values(a.write, "WRITE_SIZE", a.anchor))
+    fetch_b = 2.0 * 1024.0 * sum(f) / nf
+    write_b = 1024.0 * sum(w) / nw
     out = {"kernel": a.kernel, "config": json.loads(a.config),
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
-           "traffic_bytes_per_launch": fetch_b + write_b, "launches": [len(f), len(w)],
+           "traffic_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
+           "anchor": a.anchor,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> bytes"}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
