@@ -1641,6 +1641,8 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     // C block's LDS table; each bucket owns whole probe regions of the table
     const size_t entry = agg_entry_bytes(KW, t->naggs);
     p.uc = p.rq <= 1 ? 2 : 1;
+    if (const char *d = std::getenv("IGX_GBP_UC"))   // tuning knob: records per thread and round of pass C
+        p.uc = std::max<uint32_t>(1, std::min<uint32_t>(UCMAX, (uint32_t)std::strtoul(d, nullptr, 0)));
     const size_t stage_c = (size_t)p.uc * PTC * p.rq * 16;
     const uint32_t lb_max = std::min<uint32_t>(PART_LB_MAX, t->sbits - t->rbits);
     auto entries = [&](uint32_t lb) {
@@ -1697,13 +1699,15 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     const size_t lds_a = (size_t)TRA * (16 * p.rq + 1) + 12 * (size_t)F1 + 4 * 17;
     const size_t lds_b = (size_t)trb * (16 * p.rq + 6) + 12 * (size_t)F2 + 4 * 17;
     const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 16 + stage_c;
-    static size_t lds_set[4] = {0, 0, 0, 0};   // dynamic LDS granted to each kernel so far
-    const void *kern[4] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
+    // dynamic LDS granted to each kernel so far; pass C has a distinct-only instantiation
+    static size_t lds_set[5] = {0, 0, 0, 0, 0};
+    const void *kern[5] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_a<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_b<KW, NV>),
-                           reinterpret_cast<const void *>(k_gbp_c<KW, NV>)};
-    const size_t need[4] = {lds_k, lds_a, lds_b, lds_c};
-    for (int i = 0; i < 4; ++i) {
+                           reinterpret_cast<const void *>(k_gbp_c<KW, NV, AMAX>),
+                           reinterpret_cast<const void *>(k_gbp_c<KW, NV, 0>)};
+    const size_t need[5] = {lds_k, lds_a, lds_b, t->naggs ? lds_c : 0, t->naggs ? 0 : lds_c};
+    for (int i = 0; i < 5; ++i) {
         if (need[i] > lds_set[i]) {
             IGX_HIP(ctx, hipFuncSetAttribute(kern[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[i]));
             lds_set[i] = need[i];
@@ -1721,7 +1725,10 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
     hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
     if (p.dbg & 512u) return IGX_OK;   // ... after pass B
-    hipLaunchKernelGGL((k_gbp_c<KW, NV>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
+    if (t->naggs)
+        hipLaunchKernelGGL((k_gbp_c<KW, NV, AMAX>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
+    else   // distinct-only (C4): no aggregate decode or accumulate in the per-record path
+        hipLaunchKernelGGL((k_gbp_c<KW, NV, 0>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     return IGX_OK;
 }
 

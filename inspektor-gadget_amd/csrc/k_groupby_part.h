@@ -154,18 +154,25 @@ __device__ __forceinline__ uint64_t lds_field(const uint32_t *rec, uint32_t pos,
     return (uint64_t)rec[pos] | (w2 ? (uint64_t)rec[pos + 1] << 32 : 0ull);
 }
 
+// aggregate slots of pass C: AMAX, or 0 for a distinct-only table (no aggregates); arrays
+// keep one element so that they stay well-formed
+__host__ __device__ constexpr int nax(int na) { return na > 0 ? na : 1; }
+
 // a record in LDS -> key words, the values its aggregates add, its global event index
-template <int KW>
+template <int KW, int NA>
 __device__ __forceinline__ void lds_decode(const GbArgs &a, const PartArgs &p, const uint32_t *rec, uint32_t (&k)[KW],
-                                           uint64_t (&v)[AMAX], uint64_t &gidx) {
+                                           uint64_t (&v)[nax(NA)], uint64_t &gidx) {
     lds_key<KW>(p, rec, k);
-    uint64_t rv[AMAX], rc[AMAX];
+    v[0] = 0;
+    if constexpr (NA > 0) {
+        uint64_t rv[NA], rc[NA];
 #pragma unroll
-    for (int x = 0; x < AMAX; ++x) {
-        rv[x] = lds_field(rec, p.avp[x], p.av2[x]);
-        rc[x] = lds_field(rec, p.acp[x], p.ac2[x]);
+        for (int x = 0; x < NA; ++x) {
+            rv[x] = lds_field(rec, p.avp[x], p.av2[x]);
+            rc[x] = lds_field(rec, p.acp[x], p.ac2[x]);
+        }
+        vals_from_raw<NA>(a, rv, rc, v);
     }
-    vals_from_raw<AMAX>(a, rv, rc, v);
     const uint64_t idx = lds_field(rec, p.ipos, p.iw == 2);
     gidx = p.iw == 2 ? idx : a.base_idx + idx;
 }
@@ -668,35 +675,34 @@ __device__ __forceinline__ void wave_combine(const GbArgs &a, uint32_t rounds, b
 // C: work items from a dequeue; per item an LDS hash table, then the groups into HBM.
 // An item's records are contiguous: they are read in rounds of UC x PTC records as flat
 // 16-B quads (the next round's quads in registers while this round is aggregated from LDS).
-constexpr uint32_t UCMAX = 2;
+constexpr uint32_t UCMAX = 4;
 
-template <int KW>
+template <int KW, int NA>
 __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<KW> &T, bool ok,
                                       const uint32_t *rec) {
     uint32_t k[KW];
-    uint64_t v[AMAX], gidx = 0;
-    lds_decode<KW>(a, p, rec, k, v, gidx);
+    uint64_t v[nax(NA)], gidx = 0;
+    lds_decode<KW, NA>(a, p, rec, k, v, gidx);
     const uint64_t hh = hash_key<KW>(k);
-    if (p.combine) wave_combine<KW, AMAX>(a, p.combine, ok, k, hh, v, gidx);   // IGX_GBP_COMBINE
+    if (p.combine) wave_combine<KW, nax(NA)>(a, p.combine, ok, k, hh, v, gidx);   // IGX_GBP_COMBINE
     if (!ok || (p.dbg & 32u)) return;
     const int ei = at_find_insert<KW>(T, k, hh, p.maxp);
     if (p.dbg & 64u) return;   // diagnostics: no accumulation
     if (ei >= 0) {
 #pragma unroll
-        for (int x = 0; x < AMAX; ++x)
+        for (int x = 0; x < NA; ++x)
             if (x < (int)a.naggs && v[x])
                 atomicAdd(reinterpret_cast<unsigned long long *>(&T.agg[(uint64_t)x * T.E + ei]), (unsigned long long)v[x]);
         atomicMin(reinterpret_cast<unsigned long long *>(&T.first[ei]), (unsigned long long)gidx);
     } else {
         T.flag[0] = 1;
-        hbm_merge<KW, AMAX>(a, k, hh, v, gidx);
+        hbm_merge<KW, nax(NA)>(a, k, hh, v, gidx);
     }
 }
 
-template <int KW, int NV>
+template <int KW, int NV, int NA>
 __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
-    constexpr int NA = AMAX;
     extern __shared__ uint64_t lds[];
     AggTab<KW> T;
     const uint32_t E = p.E, rq = p.rq, uc = p.uc, RC = uc * PTC;
@@ -748,7 +754,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             if (r0 + RC < e) prefetch(r0 + RC);
             for (uint32_t u = 0; u < uc; ++u) {
                 const uint32_t i = u * PTC + threadIdx.x;
-                c_row<KW>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
+                c_row<KW, NA>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
             }
         }
         __syncthreads();
@@ -768,12 +774,13 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             uint32_t k[KW];
 #pragma unroll
             for (int q = 0; q < KW; ++q) k[q] = T.key[(uint64_t)x * KW + q];
-            uint64_t v[NA];
+            uint64_t v[nax(NA)];
+            v[0] = 0;
 #pragma unroll
             for (int q = 0; q < NA; ++q) v[q] = q < (int)a.naggs ? T.agg[(uint64_t)q * E + x] : 0ull;
             const uint64_t h = hash_key<KW>(k);
-            if (owned) flush_owned<KW, NA>(a, T, k, h, v, T.first[x], sb, p.sb_log);
-            else hbm_merge<KW, NA>(a, k, h, v, T.first[x]);
+            if (owned) flush_owned<KW, nax(NA)>(a, T, k, h, v, T.first[x], sb, p.sb_log);
+            else hbm_merge<KW, nax(NA)>(a, k, h, v, T.first[x]);
         }
         __syncthreads();
         if (owned) {
