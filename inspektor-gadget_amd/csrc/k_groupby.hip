@@ -106,7 +106,7 @@ struct GbArgs {
     uint32_t lds_entries;   // E (8 x sets)
     uint32_t direct;        // 1: probers issue their HBM atomics; the server wave probes too
     uint32_t sm;            // 1: state-machine probers (IGX_GB_PROBER=0: batch probers)
-    uint32_t admit_mask;    // 1: LDS admission on a key's second miss (ghost_admit), 0: on the first
+    uint32_t admit_mask;    // LDS admission on a key's (admit_mask + 1)-th miss (ghost_admit), 0: on the first
     uint32_t nl;            // loader waves (1..14)
     // input
     const uint8_t *valid;   // nullable: rows with 0 are skipped (nil / filtered entries)
@@ -607,8 +607,15 @@ __device__ __forceinline__ int lds_lookup(const LdsCache<KW> &c, const uint32_t 
 template <int KW>
 __device__ __forceinline__ bool ghost_admit(const GbArgs &a, const LdsCache<KW> &c, uint64_t h) {
     if (!a.admit_mask) return true;
-    const uint32_t g = (uint32_t)(h >> 20) & (GHOST - 1), t = lds_tag(h);
-    if (c.ghost[g] == t) return true;
+    // entry = tag (low 2 bits cleared) | misses seen before this one (0..3)
+    const uint32_t g = (uint32_t)(h >> 20) & (GHOST - 1), t = lds_tag(h) & ~3u;
+    const uint32_t cur = c.ghost[g];
+    if ((cur & ~3u) == t) {
+        const uint32_t seen = (cur & 3u) + 1u;
+        if (seen >= a.admit_mask) return true;
+        c.ghost[g] = t | seen;
+        return false;
+    }
     c.ghost[g] = t;   // racing writers: either tag wins, both outcomes are valid
     return false;
 }
@@ -2037,7 +2044,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.direct = 0;
     if (const char *d = std::getenv("IGX_GB_DIRECT")) a.direct = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
     if (const char *d = std::getenv("IGX_GB_PROBER")) a.sm = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
-    if (const char *d = std::getenv("IGX_GB_ADMIT")) a.admit_mask = std::strtoul(d, nullptr, 0) ? 1u : 0u;   // ablation
+    if (const char *d = std::getenv("IGX_GB_ADMIT"))   // ablation: 0 first-miss admission, k: on the (k+1)-th
+        a.admit_mask = std::min<uint32_t>(3u, (uint32_t)std::strtoul(d, nullptr, 0));
     a.dbg_cnt = t->dbg_cnt;
     const uint64_t want = (nrows + GTB - 1) / GTB;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->num_cus));
