@@ -4,6 +4,7 @@ The reference-shaped API (columns / filter / sort / group / top / gadgets) is bu
 these.  Everything here enqueues libigx.so kernels on torch's current stream.
 """
 import ctypes as C
+import os
 import math
 
 from . import _abi
@@ -132,10 +133,12 @@ def filter_rows(cols, preds, n, valid=None, any=False, nil_match=False):
     return out[:k]
 
 
-def take(tensors, idx, nrows=None):
+def take(tensors, idx, nrows=None, pad=False):
     """igx_take: rows idx (device u32/int32/int64) of every tensor ((n,) or (n, W)) gathered
     on the device into fresh tensors of the same dtypes -- the compacted batch FilterEntries
-    returns (filter.go:294-325)."""
+    returns (filter.go:294-325).  Ids >= nrows yield zero rows; pad=True marks the callers
+    that rely on it (the padded top-K merge), and IGX_DEBUG_TAKE=1 makes every other call
+    raise IndexError on such an id."""
     torch = torch_mod()
     ctx = context()
     if idx.dtype not in (torch.int32, torch.uint32):
@@ -146,6 +149,12 @@ def take(tensors, idx, nrows=None):
     outs = [torch.empty((k,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device) for t in tensors]
     if k and tensors:
         n = int(tensors[0].shape[0]) if nrows is None else nrows
+        if not pad and os.environ.get("IGX_DEBUG_TAKE"):
+            # debug assert (one host sync): igx_take zero-fills ids >= nrows, which only the
+            # padded top-K merge relies on; the torch index_select it replaced raised here
+            hi = int(idx.to(torch.int64).max())
+            if hi >= n or int(idx.to(torch.int64).min()) < 0:
+                raise IndexError(f"take: row id {hi} out of range for {n} rows")
         ccols = (Col * len(tensors))(*[col_of(t, dtype_kind(t), t[0].numel() * t.element_size() if t.dim() > 1 else None)
                                          for t in tensors])
         dst = (C.c_void_p * len(outs))(*[o.data_ptr() for o in outs])

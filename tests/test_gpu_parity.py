@@ -205,6 +205,19 @@ def test_take_rows(E, H, torch):
     assert E.take([H.to_device(cols[0])], H.to_device(np.zeros(0, np.uint32)), n)[0].numel() == 0
 
 
+def test_take_debug_assert(E, H, torch, monkeypatch):
+    """IGX_DEBUG_TAKE=1: an out-of-range row id raises IndexError (as the torch index_select
+    igx_take replaced did) unless the caller asked for zero-padded rows."""
+    col = H.to_device(np.arange(10, dtype=np.uint32))
+    idx = H.to_device(np.array([1, 12, 3], dtype=np.uint32))
+    monkeypatch.setenv("IGX_DEBUG_TAKE", "1")
+    with pytest.raises(IndexError):
+        E.take([col], idx, 10)
+    padded = E.take([col], idx, 10, pad=True)[0]
+    assert H.host(padded).tolist() == [1, 0, 3]
+    assert H.host(E.take([col], H.to_device(np.array([9, 0], dtype=np.uint32)), 10)[0]).tolist() == [9, 0]
+
+
 @pytest.mark.parametrize("spread", ["all-slots", "high-slots"])
 def test_hist_slot_window(oracle, E, H, torch, spread):
     """4096 keys x 27 slots: LDS holds a window of the slots (k_hist header); rows outside
