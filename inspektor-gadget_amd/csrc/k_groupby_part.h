@@ -125,34 +125,21 @@ __device__ __forceinline__ bool prow_ok(const GbArgs &a, uint64_t row, const PRo
 // register array is indexed by a runtime value.
 template <class L, int NV>
 __device__ __forceinline__ void prow_stage(const PartArgs &p, uint64_t row, const PRow<L, NV> &R, uint32_t *rec) {
-    // the record's words are assembled in registers (each word ORs the key columns, value
-    // halves and index words the host placed in it; the unrolled selects stay in VGPRs) and
-    // leave as whole 16-B LDS stores: no per-word LDS atomics
     constexpr int KW = L::KW;
-    constexpr int PW = part_w<KW, NV>();
-    uint64_t raw[NV > 0 ? NV : 1];
+    for (uint32_t q = 0; q < p.rq; ++q) reinterpret_cast<uint4 *>(rec)[q] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NV; ++j) raw[j] = (uint32_t)j < p.nv ? assemble(R.lo[j], R.hi[j], row * p.vcw[j], p.vcw[j]) : 0ull;
-    uint32_t w[PW];
+    for (int j = 0; j < KW; ++j)
+        if (p.kmsk[j]) atomicOr(rec + p.kpw[j], (R.k[j] & p.kmsk[j]) << p.ksh[j]);
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int j = 0; j < KW; ++j)
-            if (p.kmsk[j] && p.kpw[j] == (uint32_t)q) x |= (R.k[j] & p.kmsk[j]) << p.ksh[j];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            if ((uint32_t)j < p.nv && p.rpos[j] == (uint32_t)q) x |= (uint32_t)raw[j];
-            if ((uint32_t)j < p.nv && p.rw2[j] && p.rpos[j] + 1 == (uint32_t)q) x |= (uint32_t)(raw[j] >> 32);
+    for (int j = 0; j < NV; ++j) {
+        if ((uint32_t)j < p.nv) {
+            const uint64_t raw = assemble(R.lo[j], R.hi[j], row * p.vcw[j], p.vcw[j]);
+            rec[p.rpos[j]] = (uint32_t)raw;
+            if (p.rw2[j]) rec[p.rpos[j] + 1] = (uint32_t)(raw >> 32);
         }
-        if (p.ipos == (uint32_t)q) x |= (uint32_t)R.fi;
-        if (p.iw == 2 && p.ipos + 1 == (uint32_t)q) x |= (uint32_t)(R.fi >> 32);
-        w[q] = x;
     }
-#pragma unroll
-    for (int q = 0; q < PW / 4; ++q)
-        if ((uint32_t)q < p.rq)
-            reinterpret_cast<uint4 *>(rec)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    rec[p.ipos] = (uint32_t)R.fi;
+    if (p.iw == 2) rec[p.ipos + 1] = (uint32_t)(R.fi >> 32);
 }
 
 // the table's key words back from a record in LDS
@@ -688,7 +675,7 @@ __device__ __forceinline__ void wave_combine(const GbArgs &a, uint32_t rounds, b
 // C: work items from a dequeue; per item an LDS hash table, then the groups into HBM.
 // An item's records are contiguous: they are read in rounds of UC x PTC records as flat
 // 16-B quads (the next round's quads in registers while this round is aggregated from LDS).
-constexpr uint32_t UCMAX = 4;
+constexpr uint32_t UCMAX = 2;
 
 template <int KW, int NA>
 __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<KW> &T, bool ok,
