@@ -45,6 +45,17 @@
 
 #include "k_common.h"
 
+// event-stream loads of the group-by kernels: non-temporal (read once; IGX_GB_STREAM_NT=0
+// builds a plain-load variant for cache-residency experiments)
+#ifndef IGX_GB_STREAM_NT
+#define IGX_GB_STREAM_NT 1
+#endif
+#if IGX_GB_STREAM_NT
+#define IGX_STREAM_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define IGX_STREAM_LOAD(p) (*(p))
+#endif
+
 namespace {
 
 #ifndef IGX_GB_DIRECT_U
@@ -205,18 +216,18 @@ struct StaticLayout {
         // table's key records out of the caches
         if constexpr (w == 16) {
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + row);
+            const v4u q = IGX_STREAM_LOAD(reinterpret_cast<const v4u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y; k[o + 2] = q.z; k[o + 3] = q.w;
         } else if constexpr (w == 8) {
             typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-            const v2u q = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(p) + row);
+            const v2u q = IGX_STREAM_LOAD(reinterpret_cast<const v2u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y;
         } else if constexpr (w == 4) {
-            k[o] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p) + row);
+            k[o] = IGX_STREAM_LOAD(reinterpret_cast<const uint32_t *>(p) + row);
         } else if constexpr (w == 2) {
-            k[o] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(p) + row);
+            k[o] = IGX_STREAM_LOAD(reinterpret_cast<const uint16_t *>(p) + row);
         } else if constexpr (w == 1) {
-            k[o] = __builtin_nontemporal_load(p + row);
+            k[o] = IGX_STREAM_LOAD(p + row);
         } else {
             static_assert(w % 4 == 0, "key widths other than 1/2 must be multiples of 4");
 #pragma unroll
@@ -448,7 +459,7 @@ __device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, co
 // so each guarded column used to cost a memory round trip of its own; issued together
 // they retire under one wait.
 __device__ __forceinline__ uint32_t ldd(const uint8_t *base, uint64_t off) {
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(base + (off & ~3ull)));
+    return IGX_STREAM_LOAD(reinterpret_cast<const uint32_t *>(base + (off & ~3ull)));
 }
 
 // zero-extended value of `width` bytes from the aligned dwords lo (holding its first byte)
