@@ -41,6 +41,28 @@ PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 EV_BYTES = 71                  # saddr16 daddr16 mntns8 pid4 comm16 lport2 dport2 family2 size4 dir1
 GROUP_BYTES = 90               # key 66 + sent 8 + recv 8 + first_idx 8
 TCP_NAMES = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
+# per-config inputs (shared with tests/test_gpu_fullsize.py, which checks these exact streams)
+C3_DEVS = [(8 << 20) | (16 * k) for k in range(16)]
+C3_NCONT = 256
+C3_LOGNORMAL = (float(np.log(2e5)), 1.5)
+C4_GEN = (0xC4, 10_000, 100_000)               # seed, sources, peers
+C4_NAMES, C4_WIDTHS, C4_CAP = ("src", "pkt", "peer", "port"), [4, 1, 4, 2], 11_000_000
+C5_KEYS, C5_ZIPF, C5_TOPK = 10_000_000, 1.05, 20
+C5_NAMES, C5_WIDTHS = ("inode", "dev", "pid", "tid", "op", "count"), [8, 4, 4, 4]
+C5_CAP = C5_KEYS + C5_KEYS // 4
+
+
+def c5_aggs(A):
+    """filetop.bpf.c:68-92: reads / rbytes (op 0 = READ), writes / wbytes (op 1 = WRITE)."""
+    return [A.Agg(A.AGG_COUNT, 0, 4, 8, 0), A.Agg(A.AGG_SUM, 5, 4, 8, 0),
+            A.Agg(A.AGG_COUNT, 0, 4, 8, 1), A.Agg(A.AGG_SUM, 5, 4, 8, 1)]
+
+
+def c5_oracle_aggs(h):
+    return [{"kind": "count", "cond": h["op"], "cond_val": 0},
+            {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 0},
+            {"kind": "count", "cond": h["op"], "cond_val": 1},
+            {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 1}]
 
 
 def parse():
@@ -289,8 +311,8 @@ def run_c1(a, ctx):
 def run_c3(a, ctx):
     torch, E, H, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["D"], ctx["timer"]
     rank, world, n = ctx["rank"], ctx["world"], a.config_events
-    q = E.lognormal_quantiles(np.log(2e5), 1.5)
-    devs = [(8 << 20) | (16 * k) for k in range(16)]
+    q = E.lognormal_quantiles(*C3_LOGNORMAL)
+    devs = C3_DEVS
     ev = E.gen_bio(0xC3, H.to_device(q, ctx["dev"]), rank * n, n)
     delta = ev["delta"].view(torch.int64)
     hist = torch.zeros((4096, 27), dtype=torch.uint32, device=ctx["dev"])
@@ -300,7 +322,7 @@ def run_c3(a, ctx):
         hist.zero_()
         clk.on = record
         with clk:
-            E.hist_log2(ev["dev"], ev["cont"], delta, devs, 256, hist=hist)
+            E.hist_log2(ev["dev"], ev["cont"], delta, devs, C3_NCONT, hist=hist)
         D.allreduce_hist(hist)
 
     dt = T.run(step, a.config_steps, 1)
@@ -337,10 +359,10 @@ def run_c3(a, ctx):
 def run_c4(a, ctx):
     torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
     rank, world, n = ctx["rank"], ctx["world"], a.config_events
-    names, widths = ("src", "pkt", "peer", "port"), [4, 1, 4, 2]
-    ev = E.gen_np(0xC4, 10_000, 100_000, rank * n, n, device=ctx["dev"])   # a slice of ONE global stream
+    names, widths = C4_NAMES, C4_WIDTHS
+    ev = E.gen_np(*C4_GEN, rank * n, n, device=ctx["dev"])   # a slice of ONE global stream
     cols = [ev[k] for k in names]
-    cap = 11_000_000
+    cap = C4_CAP
     # distinct only, as the reference: graph.c:102-114 (BPF_NOEXIST, first timestamp wins),
     # advisor.go:307-319 (first event per tuple); nothing is counted
     tab = E.Table(widths, [], cap)
@@ -379,7 +401,7 @@ def run_c4(a, ctx):
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 20_000_000
-        h = O.gen_np(0xC4, 10_000, 100_000, 0, S)
+        h = O.gen_np(*C4_GEN, 0, S)
         keys = O.pad_keys(h, names)
         keep = O.np_mark(h)
         t0 = time.perf_counter()
@@ -415,14 +437,13 @@ def table_rows(E, torch, tab, fin):
 def run_c5(a, ctx):
     torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
     rank, world, n = ctx["rank"], ctx["world"], a.config_events
-    G, K = 10_000_000, 20
-    names, widths = ("inode", "dev", "pid", "tid", "op", "count"), [8, 4, 4, 4]
-    cdf_h = E.zipf_cdf(G, 1.05)
+    G, K = C5_KEYS, C5_TOPK
+    names, widths = C5_NAMES, C5_WIDTHS
+    cdf_h = E.zipf_cdf(G, C5_ZIPF)
     ev = E.gen_file(0xC5, 0, G, H.to_device(cdf_h, ctx["dev"]), rank * n, n)   # one global key universe
     cols = [ev[k] for k in names]
-    aggs = [A.Agg(A.AGG_COUNT, 0, 4, 8, 0), A.Agg(A.AGG_SUM, 5, 4, 8, 0),
-            A.Agg(A.AGG_COUNT, 0, 4, 8, 1), A.Agg(A.AGG_SUM, 5, 4, 8, 1)]
-    cap = G + G // 4
+    aggs = c5_aggs(A)
+    cap = C5_CAP
     tab = E.Table(widths, aggs, cap)
     own = E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], cap) if world > 1 else None
     clk = KernelClock(torch)
@@ -461,10 +482,7 @@ def run_c5(a, ctx):
         S = 10_000_000
         h = O.gen_file(0xC5, 0, G, cdf_h, 0, S)
         keys = O.pad_keys(h, ("inode", "dev", "pid", "tid"))
-        oaggs = [{"kind": "count", "cond": h["op"], "cond_val": 0},
-                 {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 0},
-                 {"kind": "count", "cond": h["op"], "cond_val": 1},
-                 {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 1}]
+        oaggs = c5_oracle_aggs(h)
         t0 = time.perf_counter()
         _, oa, of = O.groupby(keys, oaggs)
         perm = O.go_sort_entries([(oa[3], "uint64", True)], len(of))

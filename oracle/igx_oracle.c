@@ -655,6 +655,18 @@ static u64 group_csum(const ip_key_t *k, u64 sent, u64 recv, u64 first) {
     return mix64(h ^ (sent * 0x9E3779B97F4A7C15ull) ^ (recv * 0xC2B2AE3D27D4EB4Full) ^ (first * 0x165667B19E3779F9ull));
 }
 
+/* Order-independent fingerprint of one generic group: FNV-1a-64 over the packed key (kb
+ * bytes, the device's layout: every column padded to 4 B), then the first index and each
+ * aggregate folded in through splitmix64.  The full-table checksum is the u64 sum over groups
+ * (oracle.group_checksum is the numpy twin applied to the device table). */
+static u64 group_csum_generic(const u8 *key, u32 kb, const u64 *agg, u32 na, u64 first) {
+    u64 h = 14695981039346656037ull;
+    for (u32 i = 0; i < kb; i++) { h ^= key[i]; h *= 1099511628211ull; }
+    u64 z = h ^ (first * 0x165667B19E3779F9ull);
+    for (u32 a = 0; a < na; a++) z = mix64(z ^ (agg[a] * 0x9E3779B97F4A7C15ull));
+    return mix64(z);
+}
+
 typedef struct { mt_job *job; u32 t; } mt_arg;
 
 static inline void mt_key(const mt_job *J, u64 i, u8 *buf) {
@@ -768,10 +780,13 @@ static void *mt_worker(void *p) {
     const u64 Gt = m.n;
     map_free(&m);
     J->G[t] = Gt;
-    if (J->want_csum && !J->oom && na == 2) {
+    if (J->want_csum && !J->oom) {
         u64 cs = 0;
-        for (u64 x = 0; x < Gt; x++)
-            cs += group_csum((const ip_key_t *)(g.keys + (u64)kb * x), g.agg[x * 2], g.agg[x * 2 + 1], g.first[x]);
+        if (J->keys)
+            for (u64 x = 0; x < Gt; x++) cs += group_csum_generic(g.keys + (u64)kb * x, kb, g.agg + x * na, na, g.first[x]);
+        else
+            for (u64 x = 0; x < Gt; x++)
+                cs += group_csum((const ip_key_t *)(g.keys + (u64)kb * x), g.agg[x * 2], g.agg[x * 2 + 1], g.first[x]);
         J->csum[t] = cs;
     }
     /* phase 3: SortStats over this owner's groups (first-occurrence order), keep k */
@@ -808,8 +823,6 @@ static int cmp_u64_pair(const void *a, const void *b) {
 
 /* Returns the number of groups ((u64)-1 on allocation failure); out_first / out_agg
  * (k x naggs) receive the first k rows of the sorted groups. */
-static u64 mt_run_csum(mt_job *J, u64 *out_first, u64 *out_agg, u64 *out_csum);
-static u64 mt_run(mt_job *J, u64 *out_first, u64 *out_agg) { return mt_run_csum(J, out_first, out_agg, NULL); }
 static u64 mt_run_csum(mt_job *J, u64 *out_first, u64 *out_agg, u64 *out_csum) {
     const u32 T = J->T ? J->T : 1, na = J->naggs;
     J->T = T;
@@ -898,16 +911,18 @@ u64 or_top_tcp_mt(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 
 }
 
 /* generic keyed aggregation + top-k by aggregates (sort_agg[s], sort_desc[s] in sortBy
- * order; nsort 0 / k 0 = group count only) on T threads. */
+ * order; nsort 0 / k 0 = group count only) on T threads; out_csum (optional) receives the
+ * whole-table checksum (sum of group_csum_generic). */
 u64 or_groupby_topk_mt(const u8 *keys, u32 kb, u64 n, const u8 *valid, const or_agg *aggs, u32 naggs,
                        u64 base_idx, u32 nthreads, const u32 *sort_agg, const u32 *sort_desc, u32 nsort,
-                       u32 k, u64 *out_first, u64 *out_agg) {
+                       u32 k, u64 *out_first, u64 *out_agg, u64 *out_csum) {
     mt_job J;
     memset(&J, 0, sizeof J);
     J.keys = keys; J.kb = kb; J.valid = valid; J.aggs = aggs; J.naggs = naggs; J.n = n;
     J.base_idx = base_idx; J.T = nthreads; J.sort_agg = sort_agg; J.sort_desc = sort_desc;
     J.nsort = nsort; J.k = k;
-    return mt_run(&J, out_first, out_agg);
+    J.want_csum = out_csum != NULL;
+    return mt_run_csum(&J, out_first, out_agg, out_csum);
 }
 
 /* log2 histograms on T threads: private histograms per slice, summed (u32 wrap). */

@@ -77,7 +77,7 @@ def _declare(L):
     L.or_top_tcp_mt.argtypes = [vp] * 10 + [u64, u64, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
     L.or_top_tcp_mt.restype = u64
     L.or_groupby_topk_mt.argtypes = [vp, C.c_uint32, u64, vp, vp, C.c_uint32, u64, C.c_uint32, vp, vp,
-                                     C.c_uint32, C.c_uint32, vp, vp]
+                                     C.c_uint32, C.c_uint32, vp, vp, vp]
     L.or_groupby_topk_mt.restype = u64
     L.or_hist_log2_mt.argtypes = [vp, vp, vp, u64, vp, C.c_uint32, C.c_uint32, u64, C.c_uint32, vp,
                                   C.c_uint32]
@@ -569,6 +569,23 @@ def perm_params(G: int):
     return A % G if G > 1 else 1, 12345 % G if G > 1 else 0
 
 
+_PAR_MIN = 4_000_000
+
+
+def _par_gen(fn, head, base, n, outs, threads=None):
+    """Run a counter-based generator (event i depends only on seed and base + i) on slices of
+    [0, n) in threads; ctypes releases the GIL during each call.  Bit-identical to one call."""
+    T = threads or cpu_threads()
+    if n < _PAR_MIN or T == 1:
+        fn(*head, base, n, *[_p(o) for o in outs])
+        return
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [n * t // T for t in range(T + 1)]
+    with ThreadPoolExecutor(T) as ex:
+        list(ex.map(lambda t: fn(*head, base + cuts[t], cuts[t + 1] - cuts[t],
+                                 *[_p(o[cuts[t]:cuts[t + 1]]) for o in outs]), range(T)))
+
+
 def gen_tcp(seed, rank, G, cdf, base, n):
     A, B = perm_params(G)
     o = {
@@ -578,9 +595,8 @@ def gen_tcp(seed, rank, G, cdf, base, n):
         "dport": np.empty(n, np.uint16), "family": np.empty(n, np.uint16),
         "size": np.empty(n, np.uint32), "dir": np.empty(n, np.uint8),
     }
-    lib().or_gen_tcp(seed, rank, G, A, B, _p(cdf), base, n,
-                     *[_p(o[k]) for k in ("saddr", "daddr", "mntns", "pid", "comm", "lport",
-                                          "dport", "family", "size", "dir")])
+    _par_gen(lib().or_gen_tcp, (seed, rank, G, A, B, _p(cdf)), base, n,
+             [o[k] for k in ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")])
     return o
 
 
@@ -598,8 +614,7 @@ def gen_open(seed, comm_cdf, base, n):
 def gen_bio(seed, q, base, n):
     o = {"dev": np.empty(n, np.uint32), "cont": np.empty(n, np.uint32),
          "delta": np.empty(n, np.uint64)}
-    lib().or_gen_bio(seed, _p(q), len(q) - 1, base, n, _p(o["dev"]), _p(o["cont"]),
-                     _p(o["delta"]))
+    _par_gen(lib().or_gen_bio, (seed, _p(q), len(q) - 1), base, n, [o["dev"], o["cont"], o["delta"]])
     return o
 
 
@@ -608,9 +623,8 @@ def gen_np(seed, nsrc, npeer, base, n):
          "port": np.empty(n, np.uint16), "pkt": np.empty(n, np.uint8),
          "type": np.empty(n, np.uint8), "proto": np.empty(n, np.uint8),
          "hostip": np.empty(n, np.uint32), "raddr": np.empty(n, np.uint32)}
-    lib().or_gen_np(seed, nsrc, npeer, base, n,
-                    *[_p(o[k]) for k in ("src", "peer", "port", "pkt", "type", "proto",
-                                         "hostip", "raddr")])
+    _par_gen(lib().or_gen_np, (seed, nsrc, npeer), base, n,
+             [o[k] for k in ("src", "peer", "port", "pkt", "type", "proto", "hostip", "raddr")])
     return o
 
 
@@ -619,8 +633,8 @@ def gen_file(seed, rank, G, cdf, base, n):
     o = {"inode": np.empty(n, np.uint64), "dev": np.empty(n, np.uint32),
          "pid": np.empty(n, np.uint32), "tid": np.empty(n, np.uint32),
          "op": np.empty(n, np.uint8), "count": np.empty(n, np.uint32)}
-    lib().or_gen_file(seed, rank, G, A, B, _p(cdf), base, n,
-                      *[_p(o[k]) for k in ("inode", "dev", "pid", "tid", "op", "count")])
+    _par_gen(lib().or_gen_file, (seed, rank, G, A, B, _p(cdf)), base, n,
+             [o[k] for k in ("inode", "dev", "pid", "tid", "op", "count")])
     return o
 
 
@@ -1036,9 +1050,10 @@ def tcp_group_checksum(fields66, sent, recv, first):
         return int(z.sum(dtype=np.uint64))
 
 
-def groupby_topk_mt(keys_packed, aggs, valid=None, base_idx=0, sort=(), k=0, threads=None):
+def groupby_topk_mt(keys_packed, aggs, valid=None, base_idx=0, sort=(), k=0, threads=None, checksum=False):
     """or_groupby_topk_mt: keyed aggregation (aggs as for groupby) + the first k groups
-    sorted by [(agg index, desc)] on `threads` threads.  Returns (G, first (k,), aggs (k, naggs))."""
+    sorted by [(agg index, desc)] on `threads` threads.  Returns (G, first (k,), aggs (k, naggs)),
+    plus the whole-table checksum (group_checksum over every group) when `checksum`."""
     T = threads or cpu_threads()
     keys_packed = np.ascontiguousarray(keys_packed, dtype=np.uint8)
     n, kb = keys_packed.shape
@@ -1062,12 +1077,37 @@ def groupby_topk_mt(keys_packed, aggs, valid=None, base_idx=0, sort=(), k=0, thr
     first = np.zeros(max(1, k), np.uint64)
     out = np.zeros((max(1, k), max(1, len(aggs))), np.uint64)
     v8 = None if valid is None else np.ascontiguousarray(valid.astype(np.uint8))
+    cs = np.zeros(1, np.uint64)
     G = lib().or_groupby_topk_mt(_p(keys_packed), kb, n, _p(v8), C.cast(arr, C.c_void_p), len(cag), base_idx,
-                                 T, _p(sa), _p(sd), len(sort), k, _p(first), _p(out))
+                                 T, _p(sa), _p(sd), len(sort), k, _p(first), _p(out), _p(cs) if checksum else None)
     if G == (1 << 64) - 1:
         raise MemoryError("or_groupby_topk_mt")
     m = min(k, G)
-    return G, first[:m], out[:m, :len(aggs)]
+    res = (G, first[:m], out[:m, :len(aggs)])
+    return res + (int(cs[0]),) if checksum else res
+
+
+def group_checksum(keys, aggs, first):
+    """numpy twin of igx_oracle.c group_csum_generic summed over groups: keys (G, kb) uint8
+    in the packed layout (pad_keys), aggs a list of (G,) uint64 columns, first (G,) uint64."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    mix = lambda z: _mix64(z)   # noqa: E731
+    with np.errstate(over="ignore"):
+        h = np.full(keys.shape[0], 14695981039346656037, np.uint64)
+        for i in range(keys.shape[1]):
+            h ^= keys[:, i].astype(np.uint64)
+            h *= np.uint64(1099511628211)
+        z = h ^ (np.asarray(first, np.uint64) * np.uint64(0x165667B19E3779F9))
+        for a in aggs:
+            z = mix(z ^ (np.asarray(a, np.uint64) * np.uint64(0x9E3779B97F4A7C15)))
+        return int(mix(z).sum(dtype=np.uint64))
+
+
+def _mix64(z):
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
 
 
 def hist_log2_mt(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, threads=None):

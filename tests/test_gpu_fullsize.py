@@ -43,3 +43,106 @@ def test_c2_full_size_table_and_topk(oracle, igx, torch):
     assert dev_cs == ref_cs
     t64 = lambda o: top[:, o:o + 8].copy().view(np.uint64).ravel()    # noqa: E731
     assert np.array_equal(t64(88), first) and np.array_equal(t64(72), sent) and np.array_equal(t64(80), recv)
+
+
+# ------------------------------------------------------------------------------------
+# C3 / C4 / C5 at the bench's per-GPU size (125M events = the 8-GPU configs' 1B / 8), on the
+# exact streams, table capacities and group-by modes bench.py runs
+# ------------------------------------------------------------------------------------
+NC = 125_000_000
+
+
+def _table_check(oracle, E, H, torch, bench, tab, fin, naggs):
+    """Whole device table -> (G, checksum) with the oracle's generic group fingerprint."""
+    rows = H.host(bench.table_rows(E, torch, tab, fin))
+    kb = fin["key_bytes"]
+    u64 = lambda o: rows[:, o:o + 8].copy().view(np.uint64).ravel()   # noqa: E731
+    cs = oracle.group_checksum(rows[:, :kb], [u64(kb + 8 * a) for a in range(naggs)], u64(kb + 8 * naggs))
+    return rows.shape[0], cs
+
+
+def test_c3_full_size_histogram(oracle, igx, torch):
+    """profile block-io at 125M events: the whole u32[16*256][27] histogram equal to
+    or_hist_log2_mt (biolatency.bpf.c:100-154 per event), including the slot-window path."""
+    E, H = igx.engine, igx.columns
+    bench = importlib.import_module("bench")
+    q = E.lognormal_quantiles(*bench.C3_LOGNORMAL)
+    ev = E.gen_bio(0xC3, H.to_device(q), 0, NC)
+    hist = E.hist_log2(ev["dev"], ev["cont"], ev["delta"].view(torch.int64), bench.C3_DEVS, bench.C3_NCONT)
+    hist2 = E.hist_log2(ev["dev"], ev["cont"], ev["delta"].view(torch.int64), bench.C3_DEVS, bench.C3_NCONT,
+                        hist=hist.clone())          # accumulates onto a non-zero histogram
+    got, got2 = H.host(hist), H.host(hist2)
+    del ev
+    torch.cuda.empty_cache()
+    h = oracle.gen_bio(0xC3, q, 0, NC)
+    ref = oracle.hist_log2_mt(h["dev"], h["cont"], h["delta"], bench.C3_DEVS, bench.C3_NCONT)
+    assert int(ref.astype(np.uint64).sum()) > NC // 2
+    assert np.array_equal(got, ref)
+    assert np.array_equal(got2, (ref.astype(np.uint64) * 2).astype(np.uint32))
+
+
+def test_c4_full_size_distinct(oracle, igx, torch):
+    """advise network-policy at 125M events, cap 11M: the distinct-tuple count and a checksum
+    of every (tuple, first index) equal or_groupby_topk_mt's (advisor.go:302-320, first event
+    wins), for the bench's AUTO sequence (interval 1 cached and measured, then the
+    capacity-derived partitioned plan) and each explicit form."""
+    E, H, A = igx.engine, igx.columns, igx._abi
+    bench = importlib.import_module("bench")
+    ev = E.gen_np(*bench.C4_GEN, 0, NC)
+    cols = [ev[k] for k in bench.C4_NAMES]
+    tab = E.Table(bench.C4_WIDTHS, [], bench.C4_CAP)
+    got = []
+    for mode in (A.GB_AUTO, A.GB_AUTO, A.GB_AUTO, A.GB_CACHED, A.GB_PART, A.GB_DIRECT):
+        tab.reset()
+        tab.set_mode(mode)
+        keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
+        tab.update(cols, [0, 1, 2, 3], NC, 0, valid=keep)
+        fin = tab.finalize()
+        got.append((fin["n_groups"],) + _table_check(oracle, E, H, torch, bench, tab, fin, 0))
+    tab.destroy()
+    del ev, cols, keep
+    torch.cuda.empty_cache()
+    h = oracle.gen_np(*bench.C4_GEN, 0, NC)
+    keys = oracle.pad_keys(h, bench.C4_NAMES)
+    valid = oracle.np_mark(h)
+    del h
+    G, _, _, cs = oracle.groupby_topk_mt(keys, [], valid=valid, checksum=True)
+    assert G > 10_000_000
+    for i, (ng, nrows, dcs) in enumerate(got):
+        assert ng == nrows == G, (i, ng, nrows, G)
+        assert dcs == cs, i
+
+
+def test_c5_full_size_table_and_topk(oracle, igx, torch):
+    """top file at 125M events over 10M Zipf(1.05) keys, cap 12.5M: group count, a checksum of
+    every (key, reads, rbytes, writes, wbytes, first) and the top-20 by [-wbytes] bit-exact vs
+    or_groupby_topk_mt (filetop.bpf.c:68-92, SortStats), cached (AUTO) and partitioned."""
+    E, H, A = igx.engine, igx.columns, igx._abi
+    bench = importlib.import_module("bench")
+    cdf = E.zipf_cdf(bench.C5_KEYS, bench.C5_ZIPF)
+    ev = E.gen_file(0xC5, 0, bench.C5_KEYS, H.to_device(cdf), 0, NC)
+    cols = [ev[k] for k in bench.C5_NAMES]
+    tab = E.Table(bench.C5_WIDTHS, bench.c5_aggs(A), bench.C5_CAP)
+    got = []
+    for mode in (A.GB_AUTO, A.GB_AUTO, A.GB_PART):
+        tab.reset()
+        tab.set_mode(mode)
+        tab.update(cols, [0, 1, 2, 3], NC, 0)
+        fin = tab.finalize()
+        top = H.host(tab.gather(tab.sort([(A.TSRC_AGG, 3, True)], bench.C5_TOPK)))
+        got.append((fin["n_groups"],) + _table_check(oracle, E, H, torch, bench, tab, fin, 4) + (top,))
+    tab.destroy()
+    del ev, cols
+    torch.cuda.empty_cache()
+    h = oracle.gen_file(0xC5, 0, bench.C5_KEYS, cdf, 0, NC)
+    keys = oracle.pad_keys(h, ("inode", "dev", "pid", "tid"))
+    G, first, aggs, cs = oracle.groupby_topk_mt(keys, bench.c5_oracle_aggs(h), sort=[(3, True)],
+                                                k=bench.C5_TOPK, checksum=True)
+    assert G > 5_000_000
+    for i, (ng, nrows, dcs, top) in enumerate(got):
+        assert ng == nrows == G, (i, ng, nrows, G)
+        assert dcs == cs, i
+        t64 = lambda o: top[:, o:o + 8].copy().view(np.uint64).ravel()    # noqa: E731
+        assert np.array_equal(t64(52), first), i
+        for a in range(4):
+            assert np.array_equal(t64(20 + 8 * a), aggs[:, a]), (i, a)

@@ -1,4 +1,4 @@
-# Round-2 checkpoint: the whole -m gpu suite, smoke, then tools/gpu/profile_r02.sh.
+# Round checkpoint: the whole -m gpu suite, smoke, then tools/gpu/profile.sh <round>.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -6,4 +6,4 @@ timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
-bash tools/gpu/profile_r02.sh
+bash tools/gpu/profile.sh ${1:-r03}

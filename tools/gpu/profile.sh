@@ -1,10 +1,11 @@
-# Round-2 profile: rocprofv3 kernel trace + stats of the bench (all configs), separate
+# Per-round profile (bash tools/gpu/profile.sh r03): rocprofv3 kernel trace + stats of the bench (all configs), separate
 # FETCH_SIZE / WRITE_SIZE PMC passes -> per-config dominant-kernel traffic, and the L2
-# hit/miss + memory-side request counters of the C2 group-by.  Outputs under gpurun_out/r02/
-# (copy to profiles/r02/ afterwards).
+# hit/miss + memory-side request counters of the C2 group-by.  Outputs under gpurun_out/<round>/
+# (copy to profiles/<round>/ afterwards).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r02
+R=${1:-r03}
+O=gpurun_out/$R
 rm -rf $O; mkdir -p $O
 B="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --config-steps 3"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/trace.log 2>&1 || { echo "trace failed rc=$?"; tail $O/trace.log; exit 1; }
