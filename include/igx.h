@@ -375,9 +375,12 @@ int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32
  * IGX_DIST_ID_BYTES bytes to every rank by the caller's own channel (ncclUniqueId); every rank
  * then calls igx_dist_init on its context.  Collectives are enqueued on the context's stream
  * and must be called in the same order on every rank.  The row exchanges all-gather their
- * counts and capacities first (they synchronise the stream), so either every rank proceeds or
- * every rank returns IGX_ENOSPC.  With out == NULL on every rank they are a size query: the
- * counts are exchanged and returned, no rows move. */
+ * counts, capacities and an argument-error flag first (they synchronise the stream) and plan
+ * with igx_dist_plan_* below, so either every rank proceeds or every rank returns the same
+ * error (IGX_ENOSPC, or IGX_EINVAL when some rank's arguments are invalid).  With out == NULL
+ * on every rank they are a size query: the counts are exchanged and returned, no rows move.
+ * A failure inside the RCCL send/recv group (IGX_EIO) closes the group and marks the
+ * communicator broken: every later call on it returns IGX_EIO. */
 #define IGX_DIST_ID_BYTES 128
 typedef struct igx_dist igx_dist;
 int igx_dist_get_unique_id(uint8_t *out_id);
@@ -405,6 +408,30 @@ int igx_dist_alltoallv_rows(igx_dist *d, const void *rows, const uint64_t *send_
  * rows received. */
 int igx_dist_exchange_groups(igx_dist *d, const void *rows, uint64_t nrows, uint32_t row_bytes,
                              uint32_t key_bytes, void *out, uint64_t cap_rows, uint64_t *out_nrows);
+/* The planning step of the row exchanges, as a host function (no GPU, no communicator): every
+ * rank calls it on the same all-gathered metadata, so every rank reaches the same decision.
+ * meta holds nranks rows, rank r's row written by rank r:
+ *   igx_dist_plan_alltoallv: nranks + 2 words = send_counts[0..nranks) | cap_rows | flags
+ *   igx_dist_plan_allgather: 3 words          = nrows | cap_rows | flags
+ * flags: IGX_DIST_F_BADARG (that rank's own arguments are invalid), IGX_DIST_F_QUERY (a size
+ * query: out == NULL).  status: IGX_OK (proceed; for a query on every rank, only the counts are
+ * meaningful), IGX_EINVAL (a rank flagged BADARG, or ranks disagree on QUERY), IGX_ENOSPC (a
+ * rank's capacity is below the rows it would receive); culprit = that rank (lowest), else -1.
+ * Row offsets: send_off[p] = first row this rank sends to rank p (alltoallv; 0 for allgather);
+ * recv_off[p] / recv_counts[p] = where rank p's rows land in this rank's output and how many. */
+#define IGX_DIST_MAX_RANKS 64
+#define IGX_DIST_F_BADARG 1u
+#define IGX_DIST_F_QUERY 2u
+typedef struct {
+    int32_t status;
+    int32_t culprit;
+    uint64_t total_rows;
+    uint64_t recv_counts[IGX_DIST_MAX_RANKS];
+    uint64_t send_off[IGX_DIST_MAX_RANKS];
+    uint64_t recv_off[IGX_DIST_MAX_RANKS];
+} igx_dist_plan;
+int igx_dist_plan_alltoallv(int nranks, int rank, const uint64_t *meta, igx_dist_plan *out);
+int igx_dist_plan_allgather(int nranks, int rank, const uint64_t *meta, igx_dist_plan *out);
 
 /* The step before the path: array-of-structs records on the device (a BPF
  * map dump of {key, value} structs or perf-ring event structs, e.g. tcptopIpKeyT +

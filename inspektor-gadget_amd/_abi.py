@@ -76,6 +76,15 @@ class OpenCols(C.Structure):
 
 OPEN_SAMPLE_BYTES = 304
 DIST_ID_BYTES = 128
+DIST_MAX_RANKS = 64
+DIST_F_BADARG, DIST_F_QUERY = 1, 2
+
+
+class DistPlan(C.Structure):
+    """igx_dist_plan: the all-ranks decision and row offsets of a row exchange."""
+    _fields_ = [("status", C.c_int32), ("culprit", C.c_int32), ("total_rows", C.c_uint64),
+                ("recv_counts", C.c_uint64 * DIST_MAX_RANKS), ("send_off", C.c_uint64 * DIST_MAX_RANKS),
+                ("recv_off", C.c_uint64 * DIST_MAX_RANKS)]
 
 
 class IgxError(RuntimeError):
@@ -139,6 +148,8 @@ SIGNATURES = [
     ("igx_dist_allgather_rows", _I, [_VP, _VP, _U64, _U32, _VP, _U64, C.POINTER(_U64)]),
     ("igx_dist_alltoallv_rows", _I, [_VP, _VP, C.POINTER(_U64), _U32, _VP, _U64, C.POINTER(_U64)]),
     ("igx_dist_exchange_groups", _I, [_VP, _VP, _U64, _U32, _U32, _VP, _U64, C.POINTER(_U64)]),
+    ("igx_dist_plan_alltoallv", _I, [_I, _I, C.POINTER(_U64), C.POINTER(DistPlan)]),
+    ("igx_dist_plan_allgather", _I, [_I, _I, C.POINTER(_U64), C.POINTER(DistPlan)]),
     ("igx_ingest_open_events", _I, [_VP, _VP, _U64, _U32, C.c_int64, C.POINTER(OpenCols)]),
     ("igx_ingest_aos", _I, [_VP, _VP, _U64, _U32, C.POINTER(_U32), C.POINTER(_U32), _U32,
                             C.POINTER(_VP)]),

@@ -24,7 +24,8 @@ struct igx_dist {
     igx_ctx *ctx = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
-    uint64_t *d_meta = nullptr;   // device: own meta, then all ranks' meta
+    bool broken = false;          // an RCCL call failed inside a group: the communicator is unusable
+    uint64_t *d_meta = nullptr;   // device: own meta, then all ranks' meta (sized at init)
     uint64_t *h_meta = nullptr;   // pinned host copy of all ranks' meta
     size_t meta_words = 0;        // per-rank words the buffers hold
     uint8_t *part = nullptr;      // exchange_groups: rows grouped by owner
@@ -32,12 +33,91 @@ struct igx_dist {
     uint64_t *d_cnt = nullptr;    // exchange_groups: rows per owner
 };
 
+// the widest per-rank meta row any call gathers: alltoallv's send counts, capacity, flags
+static constexpr size_t META_WORDS = IGX_DIST_MAX_RANKS + 2;
+
 #define IGX_NCCL(d, expr)                                                                   \
     do {                                                                                    \
         ncclResult_t r_ = (expr);                                                           \
         if (r_ != ncclSuccess)                                                              \
             return igx_fail((d)->ctx, IGX_EIO, "%s: %s", #expr, ncclGetErrorString(r_));    \
     } while (0)
+// inside ncclGroupStart/End: close the group before failing, and mark the communicator broken
+// (the peers' matching sends / receives may never complete, so it must not be reused)
+#define IGX_NCCL_G(d, expr)                                                                 \
+    do {                                                                                    \
+        ncclResult_t r_ = (expr);                                                           \
+        if (r_ != ncclSuccess) {                                                            \
+            (void)ncclGroupEnd();                                                           \
+            (d)->broken = true;                                                             \
+            return igx_fail((d)->ctx, IGX_EIO, "%s: %s", #expr, ncclGetErrorString(r_));    \
+        }                                                                                   \
+    } while (0)
+
+// ---- planning (host only; tests/test_dist_plan.py checks it against gloo's all-to-all) ----
+static void plan_reset(igx_dist_plan *p) {
+    std::memset(p, 0, sizeof *p);
+    p->culprit = -1;
+}
+
+extern "C" int igx_dist_plan_alltoallv(int nranks, int rank, const uint64_t *meta, igx_dist_plan *p) {
+    if (!p || !meta || nranks < 1 || nranks > IGX_DIST_MAX_RANKS || rank < 0 || rank >= nranks) return IGX_EINVAL;
+    plan_reset(p);
+    const size_t W = (size_t)nranks + 2;
+    auto row = [&](int r) { return meta + (size_t)r * W; };
+    const uint64_t q0 = row(0)[nranks + 1] & IGX_DIST_F_QUERY;
+    for (int r = 0; r < nranks && p->culprit < 0; ++r)
+        if ((row(r)[nranks + 1] & IGX_DIST_F_BADARG) || (row(r)[nranks + 1] & IGX_DIST_F_QUERY) != q0) {
+            p->status = IGX_EINVAL;
+            p->culprit = r;
+        }
+    uint64_t soff = 0, roff = 0;
+    for (int q = 0; q < nranks; ++q) {
+        p->send_off[q] = soff;
+        soff += row(rank)[q];
+        p->recv_counts[q] = row(q)[rank];
+        p->recv_off[q] = roff;
+        roff += p->recv_counts[q];
+    }
+    p->total_rows = roff;
+    if (p->status || q0) return IGX_OK;
+    for (int dst = 0; dst < nranks; ++dst) {   // every rank sees every capacity: all fail or none does
+        uint64_t tot = 0;
+        for (int src = 0; src < nranks; ++src) tot += row(src)[dst];
+        if (tot > row(dst)[nranks]) {
+            p->status = IGX_ENOSPC;
+            p->culprit = dst;
+            break;
+        }
+    }
+    return IGX_OK;
+}
+
+extern "C" int igx_dist_plan_allgather(int nranks, int rank, const uint64_t *meta, igx_dist_plan *p) {
+    if (!p || !meta || nranks < 1 || nranks > IGX_DIST_MAX_RANKS || rank < 0 || rank >= nranks) return IGX_EINVAL;
+    plan_reset(p);
+    const uint64_t q0 = meta[2] & IGX_DIST_F_QUERY;
+    for (int r = 0; r < nranks && p->culprit < 0; ++r)
+        if ((meta[3 * r + 2] & IGX_DIST_F_BADARG) || (meta[3 * r + 2] & IGX_DIST_F_QUERY) != q0) {
+            p->status = IGX_EINVAL;
+            p->culprit = r;
+        }
+    uint64_t off = 0;
+    for (int r = 0; r < nranks; ++r) {
+        p->recv_counts[r] = meta[3 * r];
+        p->recv_off[r] = off;
+        off += meta[3 * r];
+    }
+    p->total_rows = off;
+    if (p->status || q0) return IGX_OK;
+    for (int r = 0; r < nranks; ++r)
+        if (off > meta[3 * r + 1]) {
+            p->status = IGX_ENOSPC;
+            p->culprit = r;
+            break;
+        }
+    return IGX_OK;
+}
 
 extern "C" int igx_dist_get_unique_id(uint8_t *out_id) {
     if (!out_id) return IGX_EINVAL;
@@ -55,12 +135,26 @@ extern "C" int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int ra
     IGX_HIP(ctx, hipSetDevice(ctx->device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, IGX_DIST_ID_BYTES);
+    if (nranks > IGX_DIST_MAX_RANKS)
+        return igx_fail(ctx, IGX_ENOTSUP, "dist_init: more than %d ranks", IGX_DIST_MAX_RANKS);
     auto *d = new igx_dist();
     d->ctx = ctx;
     d->rank = rank;
     d->nranks = nranks;
+    // the metadata buffers are sized once here, so no collective ever allocates (an
+    // allocation failure on one rank would leave the others waiting in the all-gather)
+    if (hipMalloc(&d->d_meta, META_WORDS * (nranks + 1) * 8) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&d->h_meta), META_WORDS * (nranks + 1) * 8, hipHostMallocDefault) !=
+            hipSuccess) {
+        (void)hipFree(d->d_meta);
+        delete d;
+        return igx_fail(ctx, IGX_ENOMEM, "dist_init: metadata buffers");
+    }
+    d->meta_words = META_WORDS;
     const ncclResult_t r = ncclCommInitRank(&d->comm, nranks, uid, rank);
     if (r != ncclSuccess) {
+        (void)hipFree(d->d_meta);
+        (void)hipHostFree(d->h_meta);
         delete d;
         return igx_fail(ctx, IGX_EIO, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
     }
@@ -87,21 +181,12 @@ extern "C" int igx_dist_rank(igx_dist *d, int *rank, int *nranks) {
     return IGX_OK;
 }
 
-// All-gather `words` u64 of host meta from every rank into d->h_meta[rank * words + i].
-// Synchronises the stream.
+// All-gather `words` (<= META_WORDS) u64 of host meta from every rank into
+// d->h_meta[rank * words + i].  Synchronises the stream.  Allocates nothing.
 static int gather_meta(igx_dist *d, const uint64_t *mine, size_t words) {
     igx_ctx *ctx = d->ctx;
-    if (words > d->meta_words) {
-        (void)hipFree(d->d_meta);
-        (void)hipHostFree(d->h_meta);
-        d->d_meta = nullptr;
-        d->h_meta = nullptr;
-        d->meta_words = 0;
-        IGX_HIP(ctx, hipMalloc(&d->d_meta, words * (d->nranks + 1) * 8));
-        IGX_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&d->h_meta), words * (d->nranks + 1) * 8,
-                                   hipHostMallocDefault));
-        d->meta_words = words;
-    }
+    if (d->broken) return igx_fail(ctx, IGX_EIO, "dist: communicator broken by an earlier failure");
+    if (words > d->meta_words) return igx_fail(ctx, IGX_EINVAL, "dist: %zu meta words", words);
     uint64_t *h_send = d->h_meta + words * d->nranks;   // the spare row of the pinned buffer
     std::memcpy(h_send, mine, words * 8);
     IGX_HIP(ctx, hipMemcpyAsync(d->d_meta, h_send, words * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -110,6 +195,13 @@ static int gather_meta(igx_dist *d, const uint64_t *mine, size_t words) {
                                 ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return IGX_OK;
+}
+
+static int plan_fail(igx_dist *d, const igx_dist_plan &p, const char *what) {
+    if (p.status == IGX_ENOSPC)
+        return igx_fail(d->ctx, IGX_ENOSPC, "%s: %llu rows exceed rank %d's capacity", what,
+                        (unsigned long long)p.total_rows, p.culprit);
+    return igx_fail(d->ctx, p.status, "%s: invalid arguments on rank %d", what, p.culprit);
 }
 
 extern "C" int igx_dist_allreduce_u32(igx_dist *d, uint32_t *buf, uint64_t n) {
@@ -133,32 +225,28 @@ extern "C" int igx_dist_allgather_rows(igx_dist *d, const void *rows, uint64_t n
                                        void *out, uint64_t cap_rows, uint64_t *counts) {
     if (!d) return IGX_EINVAL;
     igx_ctx *ctx = d->ctx;
-    if (row_bytes == 0) return igx_fail(ctx, IGX_EINVAL, "dist_allgather: zero row width");
-    const uint64_t mine[2] = {nrows, cap_rows};
-    int rc = gather_meta(d, mine, 2);
+    // local argument checks travel with the counts, so a bad call fails on every rank
+    const bool bad = row_bytes == 0 || (out && nrows && !rows);
+    const uint64_t mine[3] = {nrows, cap_rows, (bad ? IGX_DIST_F_BADARG : 0u) | (out ? 0u : IGX_DIST_F_QUERY)};
+    int rc = gather_meta(d, mine, 3);
     if (rc) return rc;
+    igx_dist_plan p;
+    (void)igx_dist_plan_allgather(d->nranks, d->rank, d->h_meta, &p);
+    if (p.status) return plan_fail(d, p, "dist_allgather");
     const int nr = d->nranks;
-    std::vector<uint64_t> cnt(nr), off(nr + 1, 0);
-    for (int r = 0; r < nr; ++r) {
-        cnt[r] = d->h_meta[2 * r];
-        off[r + 1] = off[r] + cnt[r];
-    }
-    if (counts) std::memcpy(counts, cnt.data(), nr * 8);
+    if (counts) std::memcpy(counts, p.recv_counts, nr * 8);
     if (!out) return IGX_OK;   // size query (every rank passes a NULL out)
-    for (int r = 0; r < nr; ++r)   // every rank sees every capacity: all fail or none does
-        if (off[nr] > d->h_meta[2 * r + 1])
-            return igx_fail(ctx, IGX_ENOSPC, "dist_allgather: %llu rows exceed rank %d's capacity %llu",
-                            (unsigned long long)off[nr], r, (unsigned long long)d->h_meta[2 * r + 1]);
-    if (nrows && !rows) return igx_fail(ctx, IGX_EINVAL, "dist_allgather: null rows");
     auto *o = static_cast<uint8_t *>(out);
     if (nrows)
-        IGX_HIP(ctx, hipMemcpyAsync(o + off[d->rank] * row_bytes, rows, nrows * row_bytes, hipMemcpyDeviceToDevice,
-                                    ctx->stream));
+        IGX_HIP(ctx, hipMemcpyAsync(o + p.recv_off[d->rank] * row_bytes, rows, nrows * row_bytes,
+                                    hipMemcpyDeviceToDevice, ctx->stream));
     IGX_NCCL(d, ncclGroupStart());
-    for (int p = 0; p < nr; ++p) {
-        if (p == d->rank) continue;
-        if (nrows) IGX_NCCL(d, ncclSend(rows, nrows * row_bytes, ncclUint8, p, d->comm, ctx->stream));
-        if (cnt[p]) IGX_NCCL(d, ncclRecv(o + off[p] * row_bytes, cnt[p] * row_bytes, ncclUint8, p, d->comm, ctx->stream));
+    for (int q = 0; q < nr; ++q) {
+        if (q == d->rank) continue;
+        if (nrows) IGX_NCCL_G(d, ncclSend(rows, nrows * row_bytes, ncclUint8, q, d->comm, ctx->stream));
+        if (p.recv_counts[q])
+            IGX_NCCL_G(d, ncclRecv(o + p.recv_off[q] * row_bytes, p.recv_counts[q] * row_bytes, ncclUint8, q, d->comm,
+                                   ctx->stream));
     }
     IGX_NCCL(d, ncclGroupEnd());
     return IGX_OK;
@@ -169,45 +257,31 @@ extern "C" int igx_dist_alltoallv_rows(igx_dist *d, const void *rows, const uint
     if (!d) return IGX_EINVAL;
     igx_ctx *ctx = d->ctx;
     const int nr = d->nranks;
-    if (row_bytes == 0 || !send_counts) return igx_fail(ctx, IGX_EINVAL, "dist_alltoallv: bad arguments");
-    std::vector<uint64_t> mine(nr + 1);
-    for (int p = 0; p < nr; ++p) mine[p] = send_counts[p];
+    uint64_t mine[META_WORDS] = {};
+    uint64_t nsend = 0;
+    for (int q = 0; q < nr && send_counts; ++q) nsend += (mine[q] = send_counts[q]);
     mine[nr] = cap_rows;
-    int rc = gather_meta(d, mine.data(), nr + 1);
+    const bool bad = row_bytes == 0 || !send_counts || (out && nsend && !rows);
+    mine[nr + 1] = (bad ? IGX_DIST_F_BADARG : 0u) | (out ? 0u : IGX_DIST_F_QUERY);
+    int rc = gather_meta(d, mine, nr + 2);
     if (rc) return rc;
-    const uint64_t *M = d->h_meta;   // M[src * (nr + 1) + dst], caps at column nr
-    if (!out) {   // size query (every rank passes a NULL out)
-        if (recv_counts)
-            for (int p = 0; p < nr; ++p) recv_counts[p] = M[p * (nr + 1) + d->rank];
-        return IGX_OK;
-    }
-    for (int dst = 0; dst < nr; ++dst) {
-        uint64_t tot = 0;
-        for (int src = 0; src < nr; ++src) tot += M[src * (nr + 1) + dst];
-        if (tot > M[dst * (nr + 1) + nr])
-            return igx_fail(ctx, IGX_ENOSPC, "dist_alltoallv: %llu rows exceed rank %d's capacity %llu",
-                            (unsigned long long)tot, dst, (unsigned long long)M[dst * (nr + 1) + nr]);
-    }
-    std::vector<uint64_t> soff(nr + 1, 0), roff(nr + 1, 0);
-    for (int p = 0; p < nr; ++p) {
-        soff[p + 1] = soff[p] + send_counts[p];
-        roff[p + 1] = roff[p] + M[p * (nr + 1) + d->rank];
-    }
-    if (recv_counts)
-        for (int p = 0; p < nr; ++p) recv_counts[p] = roff[p + 1] - roff[p];
-    if (soff[nr] && !rows) return igx_fail(ctx, IGX_EINVAL, "dist_alltoallv: null rows");
+    igx_dist_plan p;
+    (void)igx_dist_plan_alltoallv(nr, d->rank, d->h_meta, &p);
+    if (p.status) return plan_fail(d, p, "dist_alltoallv");
+    if (recv_counts) std::memcpy(recv_counts, p.recv_counts, nr * 8);
+    if (!out) return IGX_OK;   // size query (every rank passes a NULL out)
     const auto *s = static_cast<const uint8_t *>(rows);
     auto *o = static_cast<uint8_t *>(out);
     const uint64_t self = send_counts[d->rank];
     if (self)
-        IGX_HIP(ctx, hipMemcpyAsync(o + roff[d->rank] * row_bytes, s + soff[d->rank] * row_bytes, self * row_bytes,
-                                    hipMemcpyDeviceToDevice, ctx->stream));
+        IGX_HIP(ctx, hipMemcpyAsync(o + p.recv_off[d->rank] * row_bytes, s + p.send_off[d->rank] * row_bytes,
+                                    self * row_bytes, hipMemcpyDeviceToDevice, ctx->stream));
     IGX_NCCL(d, ncclGroupStart());
-    for (int p = 0; p < nr; ++p) {
-        if (p == d->rank) continue;
-        const uint64_t sc = send_counts[p], rcv = roff[p + 1] - roff[p];
-        if (sc) IGX_NCCL(d, ncclSend(s + soff[p] * row_bytes, sc * row_bytes, ncclUint8, p, d->comm, ctx->stream));
-        if (rcv) IGX_NCCL(d, ncclRecv(o + roff[p] * row_bytes, rcv * row_bytes, ncclUint8, p, d->comm, ctx->stream));
+    for (int q = 0; q < nr; ++q) {
+        if (q == d->rank) continue;
+        const uint64_t sc = send_counts[q], rcv = p.recv_counts[q];
+        if (sc) IGX_NCCL_G(d, ncclSend(s + p.send_off[q] * row_bytes, sc * row_bytes, ncclUint8, q, d->comm, ctx->stream));
+        if (rcv) IGX_NCCL_G(d, ncclRecv(o + p.recv_off[q] * row_bytes, rcv * row_bytes, ncclUint8, q, d->comm, ctx->stream));
     }
     IGX_NCCL(d, ncclGroupEnd());
     return IGX_OK;
@@ -218,30 +292,40 @@ extern "C" int igx_dist_exchange_groups(igx_dist *d, const void *rows, uint64_t 
     if (!d) return IGX_EINVAL;
     igx_ctx *ctx = d->ctx;
     const int nr = d->nranks;
-    if (nr > 64) return igx_fail(ctx, IGX_ENOTSUP, "dist_exchange_groups: more than 64 ranks");
+    // a local failure (allocation, partition) must not skip the all-to-all's metadata
+    // exchange, or the other ranks wait in it forever: it is reported as a bad argument there,
+    // so every rank fails together
+    int lerr = IGX_OK;
     const size_t need = (size_t)nrows * row_bytes;
     if (need > d->part_bytes) {
-        IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(d->part);
         d->part = nullptr;
         d->part_bytes = 0;
-        IGX_HIP(ctx, hipMalloc(&d->part, igx_align(std::max<size_t>(need, 1), 1 << 20)));
-        d->part_bytes = igx_align(std::max<size_t>(need, 1), 1 << 20);
+        if (hipMalloc(&d->part, igx_align(std::max<size_t>(need, 1), 1 << 20)) == hipSuccess)
+            d->part_bytes = igx_align(std::max<size_t>(need, 1), 1 << 20);
+        else
+            lerr = IGX_ENOMEM;
     }
-    if (!d->d_cnt) IGX_HIP(ctx, hipMalloc(&d->d_cnt, 64 * 8));
-    uint64_t cnt[64] = {};
-    if (nrows) {
-        int rc = igx_partition_rows(ctx, static_cast<const uint8_t *>(rows), nrows, row_bytes, key_bytes,
-                                    (uint32_t)nr, d->part, d->d_cnt);
-        if (rc) return rc;
-        IGX_HIP(ctx, hipMemcpyAsync(cnt, d->d_cnt, nr * 8, hipMemcpyDeviceToHost, ctx->stream));
-        IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (!lerr && !d->d_cnt && hipMalloc(&d->d_cnt, IGX_DIST_MAX_RANKS * 8) != hipSuccess) lerr = IGX_ENOMEM;
+    uint64_t cnt[IGX_DIST_MAX_RANKS] = {};
+    if (!lerr && nrows) {
+        lerr = igx_partition_rows(ctx, static_cast<const uint8_t *>(rows), nrows, row_bytes, key_bytes, (uint32_t)nr,
+                                  d->part, d->d_cnt);
+        if (!lerr && (hipMemcpyAsync(cnt, d->d_cnt, nr * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                      hipStreamSynchronize(ctx->stream) != hipSuccess))
+            lerr = IGX_EIO;
     }
-    uint64_t rc_[64] = {};
+    uint64_t rc_[IGX_DIST_MAX_RANKS] = {};
+    if (lerr) {
+        const uint64_t zero[IGX_DIST_MAX_RANKS] = {};
+        (void)igx_dist_alltoallv_rows(d, nullptr, zero, 0 /* flags this rank BADARG */, out, cap_rows, rc_);
+        return igx_fail(ctx, lerr, "dist_exchange_groups: local failure on rank %d (%d)", d->rank, lerr);
+    }
     int rc = igx_dist_alltoallv_rows(d, d->part, cnt, row_bytes, out, cap_rows, rc_);
     if (rc) return rc;
     uint64_t tot = 0;
-    for (int p = 0; p < nr; ++p) tot += rc_[p];
+    for (int q = 0; q < nr; ++q) tot += rc_[q];
     if (out_nrows) *out_nrows = tot;
     return IGX_OK;
 }

@@ -1835,7 +1835,18 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
 // one update over layout L in the interval's form
 template <class L>
 static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
-    if (t->interval_part) return launch_part<L>(t, ctx, a);
+    if (t->interval_part) {
+        const GbArgs saved = a;   // launch_part turns the fused predicates into a row mask
+        const int rc = launch_part<L>(t, ctx, a);
+        if (rc != IGX_ENOMEM || t->mode != IGX_GB_AUTO) return rc;
+        // AUTO picked the partitioned form on its own and its scratch does not fit: this
+        // update runs cached instead (the forms share the table protocol, so they may mix
+        // within an interval), and AUTO measures again at the next interval
+        (void)hipGetLastError();
+        t->interval_part = false;
+        t->direct_left = 0;
+        a = saved;
+    }
     if (t->interval_direct) launch_direct<L>(ctx, a);
     else launch_gb<L>(ctx, a, blocks);
     return IGX_OK;

@@ -592,6 +592,10 @@ __device__ __forceinline__ void flush_owned(const GbArgs &a, const AggTab<KW> &T
         atomicOr(a.err, 32u);
         return;
     }
+    if (f >= READY_IDX) {   // an index column value that `ready` cannot carry (as find_or_insert)
+        atomicOr(a.err, 8u);
+        return;
+    }
     for (uint32_t probe = 0; probe < a.max_probe; ++probe, s = next_slot(a, s)) {
         const uint32_t l = (uint32_t)(s - sb), wd = l >> 5, bit = 1u << (l & 31);
         if (T.occ_new[wd] & bit) continue;   // claimed by another group of this flush

@@ -20,10 +20,12 @@
 // XCD (blockIdx % 8, speed only) and sweep the same chunks, so the repeated reads are L2
 // hits.  Slot window: when all keys x nslots do not fit one partition but keys x W slots
 // do (W >= 8), LDS holds only slots [lo, lo + W) of every key and rows outside the window
-// add to HBM directly (u32 atomics, still exact); lo is picked on the device by a one-
-// workgroup pass over a 64K-row sample (the window with the most rows), so no row is read
-// twice and no host round trip is added.  Latency histograms are narrow in log2 space (C3:
-// lognormal, sigma = 2.2 slots), so the window holds all but ~1e-4 of the rows.
+// add to HBM directly (u32 atomics, still exact).  Each workgroup picks its own lo from the
+// rows of its first chunk, which it loads anyway (2 rows per lane, 2048 per workgroup: the
+// window with the most of them); windows may differ between workgroups because each commits
+// its own LDS counters at its own lo, so no extra pass, kernel or host round trip is needed.
+// Latency histograms are narrow in log2 space (C3: lognormal, sigma = 2.2 slots), so the
+// window holds all but ~1e-4 of the rows.
 // Each lane keeps 8 rows (128 B of loads) in flight per chunk -- the kernel is
 // bound by bytes in flight, not by arithmetic.  Small histograms are replicated per wave
 // to spread LDS atomic contention.  Commit: one HBM atomic add per non-zero counter.
@@ -52,7 +54,6 @@ struct HistArgs {
     uint32_t single;            // ndev == 0: every row is device 0 (the shipped gadget)
     uint32_t ndev, ncont, nslots;
     uint32_t W;                 // slots held in LDS per key (== nslots without a window)
-    const uint32_t *lo;         // device: first LDS slot (null: 0)
     uint32_t P;                 // key partitions
     uint32_t Kp;                // keys per partition
     uint32_t R;                 // LDS replicas
@@ -70,6 +71,35 @@ __device__ __forceinline__ uint64_t divide(uint64_t v, uint64_t d) {
     else if constexpr (DIV == 1000000) return v / 1000000ull;
     else if constexpr (DIV == 1) return v;
     else return v / d;
+}
+
+template <int DIV>
+__device__ __forceinline__ uint32_t slot_of(int64_t d, uint64_t divisor, uint32_t nslots) {
+    const uint64_t v = divide<DIV>((uint64_t)d, divisor);
+    const uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
+    return min(slot, nslots - 1);
+}
+
+// Slot window start from this workgroup's sample: wcnt[slot] holds the sampled rows per slot;
+// wave 0 scores every candidate lo (lane l: rows in [l, l + W)) and takes the best, lowest lo
+// on ties.  Called by every thread (barriers inside).
+__device__ __forceinline__ uint32_t pick_window(uint32_t *wcnt, uint32_t *s_lo, uint32_t nslots, uint32_t W) {
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        uint32_t sum = 0;
+        if (l + W <= nslots)
+            for (uint32_t j = 0; j < W; ++j) sum += wcnt[l + j];
+        uint64_t key = ((uint64_t)sum << 8) | (63u - l);
+        if (l + W > nslots) key = 0;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t other = __shfl_xor(key, o);
+            key = other > key ? other : key;
+        }
+        if (l == 0) *s_lo = 63u - (uint32_t)(key & 0xFF);
+    }
+    __syncthreads();
+    return *s_lo;
 }
 
 template <int DIV>
@@ -94,9 +124,7 @@ struct Counter {
         if (d < 0) return;
         const uint32_t kk = di * a.ncont + ci - kbase;
         if (kk >= a.Kp) return;      // another partition's key
-        const uint64_t v = divide<DIV>((uint64_t)d, a.divisor);
-        uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
-        slot = min(slot, a.nslots - 1);
+        const uint32_t slot = slot_of<DIV>(d, a.divisor, a.nslots);
         const uint32_t ws = slot - lo;
         if (ws >= a.W) {             // outside the LDS window: straight to HBM
             atomicAdd(&a.hist[((uint64_t)kbase + kk) * a.nslots + slot], 1u);
@@ -117,17 +145,22 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     extern __shared__ uint32_t h[];
     __shared__ uint32_t skey[DEVTAB];
     __shared__ uint8_t sidx[DEVTAB];
+    __shared__ uint32_t wcnt[64];
+    __shared__ uint32_t s_lo;
     for (uint32_t i = threadIdx.x; i < a.rep_words * a.R; i += TB) h[i] = 0;
     if (threadIdx.x < DEVTAB) {
         skey[threadIdx.x] = a.dev_key[threadIdx.x];
         sidx[threadIdx.x] = a.dev_idx[threadIdx.x];
     }
+    if (threadIdx.x < 64) wcnt[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const uint32_t p = j % a.P, g = j / a.P;
     const uint32_t cgroup = g * 8 + xcd;
-    const uint32_t lo = a.lo ? *a.lo : 0u;
-    const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp, lo};
+    const bool window = a.W < a.nslots;
+    auto sample = [&](int64_t d) {
+        if (d >= 0) atomicAdd(&wcnt[slot_of<DIV>(d, a.divisor, a.nslots)], 1u);
+    };
     const uint64_t nchunks = (a.n + CHUNK - 1) / CHUNK;
     uint32_t it = 0;
     // full chunks: 8 rows per lane as 16-B loads (lane t covers rows base + 4t .. +3 and
@@ -151,9 +184,16 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     };
     const uint64_t nfull = VEC ? a.n / CHUNK : 0;
     uint64_t c = cgroup;
+    uint32_t lo = 0;
     if (c < nfull) {
         Rows R;
         load(c * CHUNK, R);
+        if (window) {
+            sample(R.d0.x);
+            sample(R.d2.x);
+            lo = pick_window(wcnt, &s_lo, a.nslots, a.W);
+        }
+        const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp, lo};
         for (; c < nfull; c += a.ngroups) {
             const Rows cur = R;
             if (c + a.ngroups < nfull) load((c + a.ngroups) * CHUNK, R);
@@ -168,7 +208,17 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
             if (++it % CHUNKS_PER_TILE == 0) __syncthreads();   // tile boundary (see header)
         }
     }
-    // the rest (partial chunk, or every chunk when the columns are not 16-B aligned)
+    // the rest (partial chunk, or every chunk when the columns are not 16-B aligned); a
+    // workgroup that starts here samples its first chunk's rows for the window
+    if (window && cgroup >= nfull) {
+        if (c < nchunks)
+            for (int r = 0; r < 2; ++r) {
+                const uint64_t row = c * CHUNK + (uint64_t)r * (CHUNK / 2) + threadIdx.x;
+                if (row < a.n) sample(a.delta[row]);
+            }
+        lo = pick_window(wcnt, &s_lo, a.nslots, a.W);
+    }
+    const Counter<DIV> count{a, skey, sidx, h + ((threadIdx.x >> 6) % a.R) * a.rep_words, p * a.Kp, lo};
     for (; c < nchunks; c += a.ngroups) {
         const uint64_t base = c * CHUNK;
 #pragma unroll
@@ -189,35 +239,6 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     }
 }
 
-// The slot window's start: log2 slots of a strided 64K-row sample (devices and containers
-// ignored), then the lo in [0, nslots - W] whose window holds the most sampled rows.
-template <int DIV>
-__global__ __launch_bounds__(TB) void k_hist_window(const int64_t *__restrict__ delta, uint64_t n, uint64_t divisor,
-                                                    uint32_t nslots, uint32_t W, uint32_t *__restrict__ lo_out) {
-    __shared__ uint32_t cnt[64];
-    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t ns = n < 65536 ? n : 65536;
-    const uint64_t step = n / ns;
-    for (uint64_t i = threadIdx.x; i < ns; i += TB) {
-        const int64_t d = delta[i * step];
-        if (d < 0) continue;
-        const uint64_t v = divide<DIV>((uint64_t)d, divisor);
-        uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
-        atomicAdd(&cnt[min(slot, nslots - 1)], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t best = 0, bsum = 0;
-        for (uint32_t l = 0; l + W <= nslots; ++l) {
-            uint32_t sum = 0;
-            for (uint32_t j = 0; j < W; ++j) sum += cnt[l + j];
-            if (sum > bsum) { bsum = sum; best = l; }
-        }
-        *lo_out = best;
-    }
-}
-
 template <int DIV>
 void launch(const HistArgs &a, uint32_t blocks, size_t lds, hipStream_t s, bool vec) {
     static bool attr_set = false;
@@ -228,8 +249,6 @@ void launch(const HistArgs &a, uint32_t blocks, size_t lds, hipStream_t s, bool 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BUDGET);
         attr_set = true;
     }
-    if (a.lo) hipLaunchKernelGGL((k_hist_window<DIV>), dim3(1), dim3(TB), 0, s, a.delta, a.n, a.divisor, a.nslots,
-                                 a.W, const_cast<uint32_t *>(a.lo));
     if (vec) hipLaunchKernelGGL((k_hist<DIV, true>), dim3(blocks), dim3(TB), lds, s, a);
     else hipLaunchKernelGGL((k_hist<DIV, false>), dim3(blocks), dim3(TB), lds, s, a);
 }
@@ -268,13 +287,7 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
     const uint64_t nkeys = (uint64_t)a.ndev * ncont;
     a.W = nslots;
     const uint64_t wfit = (LDS_BUDGET - 64) / (2ull * nkeys);   // slots per key for one partition
-    if (wfit < nslots && wfit >= 8 && !std::getenv("IGX_HIST_NOWINDOW")) {
-        a.W = (uint32_t)wfit;
-        void *sc;
-        int rc = igx_scratch(ctx, 256, &sc);
-        if (rc) return rc;
-        a.lo = static_cast<const uint32_t *>(sc);
-    }
+    if (wfit < nslots && wfit >= 8 && !std::getenv("IGX_HIST_NOWINDOW")) a.W = (uint32_t)wfit;
     const uint64_t keys_fit = (LDS_BUDGET - 64) / (2ull * a.W);
     a.P = (uint32_t)((nkeys + keys_fit - 1) / keys_fit);
     a.Kp = (uint32_t)((nkeys + a.P - 1) / a.P);

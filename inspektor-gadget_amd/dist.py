@@ -2,11 +2,12 @@
 
 One process per GPU.  Two transports carry the exchanges:
 
-  * RCCL through libigx.so's igx_dist_* C ABI (the same entry points a cgo caller binds):
-    used whenever the torch process group's backend is "nccl" (= RCCL over xGMI on MI355X).
-    torch.distributed only hands rank 0's ncclUniqueId to the other ranks.
-  * torch.distributed otherwise ("gloo": the CPU tests, and the ranks that share one GPU in
-    the world-size-2 GPU test); device tensors are staged through the host for gloo.
+  * torch.distributed (default): on an "nccl" group its collectives are RCCL over xGMI on
+    MI355X; on "gloo" (the CPU tests, and the ranks that share one GPU in the world-size-2
+    GPU test) device tensors are staged through the host.
+  * RCCL through libigx.so's igx_dist_* C ABI (the same entry points a cgo caller binds),
+    with IGX_DIST=igx on an "nccl" group; torch.distributed only hands rank 0's ncclUniqueId
+    to the other ranks.
 
 Only data movement and bookkeeping live here; every aggregation and merge runs in libigx.so:
 
@@ -159,14 +160,18 @@ class IgxComm:
 
 
 def comm():
-    """The transport for the current process group (None without one).  IGX_DIST=torch
-    forces torch.distributed on an nccl group (diagnostics)."""
+    """The transport for the current process group (None without one).  Default: torch's own
+    collectives on the group (on an "nccl" group these are RCCL over xGMI too); IGX_DIST=igx
+    selects the igx_dist_* C ABI on an nccl group.  The C-ABI exchanges' planning
+    (igx_dist_plan_*) is tested for 2..8 ranks against gloo (tests/test_dist_plan.py), but
+    their RCCL send/recv loops have only run with one rank (no multi-GPU box so far), so
+    they stay opt-in until a world >= 2 run on GPUs has checked them."""
     global _comm
     d = _dist()
     if d is None or d.get_world_size() == 1:
         return None
     if _comm is None:
-        use_igx = d.get_backend() == "nccl" and os.environ.get("IGX_DIST", "igx") != "torch"
+        use_igx = d.get_backend() == "nccl" and os.environ.get("IGX_DIST", "torch") == "igx"
         _comm = IgxComm(d) if use_igx else TorchComm(d)
     return _comm
 

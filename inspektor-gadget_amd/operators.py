@@ -324,11 +324,43 @@ class StatsParser:
     def SetEventCallback(self, cb):
         self.eventCallbackArray = cb
 
-    def _batch(self, stats):
+    def _parser_for(self, stats):
+        """The parser for this batch: the configured one, or -- when a string value is longer
+        than its column's declared width -- one over a copy of the schema whose string columns
+        are as wide as the batch's longest value (Go compares whole strings, parser.go:209-221:
+        a path or pod name must not be cut to the column width before MatchAll / Sort)."""
+        from . import columns as _c
+        from . import parser as _p
+        wide = {}
+        for c in self.cols.GetOrderedColumns():
+            attr = self.attr.get(c.Name.lower())
+            if c.kind == "string" and not c.virtual and attr:
+                m = max((len(str(getattr(s, attr)).encode()) for s in stats), default=0)
+                if m > c.width:
+                    wide[c.Name.lower()] = (m + 7) // 8 * 8
+        if not wide:
+            return self.cols, self.p
+        key = tuple(sorted(wide.items()))
+        cache = self.__dict__.setdefault("_wide", {})
+        if key not in cache:
+            cols = _c.Columns()
+            for c in self.cols.GetOrderedColumns():
+                cols._add(_c.Column(c.Name, c.kind, wide.get(c.Name.lower(), c.width), c.GroupType, c.virtual,
+                                    c.extractor))
+            p = _p.NewParser(cols)
+            if self.p.filters:
+                p.SetFilters(self.p.filters)
+            if self.p.sortSpec is not None:
+                p.SetSorting(self.p.sortBy)
+            cache[key] = (cols, p)
+        return cache[key]
+
+    def _batch(self, stats, cols=None):
         import numpy as np
         from . import columns as H
+        cols = self.cols if cols is None else cols
         data = {}
-        for c in self.cols.GetOrderedColumns():
+        for c in cols.GetOrderedColumns():
             if c.virtual:
                 continue
             name = c.Name.lower()
@@ -348,7 +380,7 @@ class StatsParser:
                 a = np.array([getattr(s, attr) if attr else 0 for s in stats], dt)
             data[name] = H.to_device(a)
         data["__row"] = H.to_device(np.arange(len(stats), dtype=np.int32))
-        return H.EventBatch(self.cols, data)
+        return H.EventBatch(cols, data)
 
     def EventHandlerFuncArray(self, *enrichers):
         from . import columns as H
@@ -359,11 +391,12 @@ class StatsParser:
                     e(s)
             out = stats
             if stats and (self.p.filterSpecs is not None or self.p.sortSpec is not None):
-                b = self._batch(stats)
-                if self.p.filterSpecs is not None:
-                    b = b.take(self.p.filterSpecs.MatchAll(b))
-                if self.p.sortSpec is not None and b.n:
-                    b = self.p.sortSpec.Sort(b)
+                cols, p = self._parser_for(stats)
+                b = self._batch(stats, cols)
+                if p.filterSpecs is not None:
+                    b = b.take(p.filterSpecs.MatchAll(b))
+                if p.sortSpec is not None and b.n:
+                    b = p.sortSpec.Sort(b)
                 out = [stats[int(i)] for i in H.host(b["__row"])] if b.n else []
             if self.eventCallbackArray is not None:
                 self.eventCallbackArray(out)

@@ -76,6 +76,11 @@ def test_igx_dist_rccl_single_rank(igx, torch, oracle):
                                             1000, rc))
         torch.cuda.synchronize()
         assert torch.equal(out2, rows)
+        # an argument error (null rows with rows to send) fails through the plan, and leaves
+        # the communicator usable
+        assert L.igx_dist_alltoallv_rows(h, None, sc, 96, C.c_void_p(out2.data_ptr()), 1000, rc) == A.IGX_EINVAL
+        assert L.igx_dist_allgather_rows(h, C.c_void_p(rows.data_ptr()), 1000, 0, C.c_void_p(out.data_ptr()),
+                                         1000, cnt) == A.IGX_EINVAL
         got = C.c_uint64()
         out3 = torch.empty_like(rows)
         ctx.check(L.igx_dist_exchange_groups(h, C.c_void_p(rows.data_ptr()), 1000, 96, 72,

@@ -69,3 +69,41 @@ def test_profile_block_io_through_runtime(oracle, igx, torch):
     slots = oracle.hist_log2(None, None, h["delta"], [], 1)[0] * 3
     exp = oracle.get_report(slots)
     assert [d["count"] for d in rep["data"]] == [d["count"] for d in exp]
+
+
+def test_stats_parser_long_strings(oracle, igx, torch):
+    """Pod names longer than the column's 64 bytes that share their first 80 bytes: the Go
+    parser filters and sorts on the whole string (parser.go:209-221), so a regex on the tail
+    and a sort by pod must see past the declared width (operators.StatsParser widens the batch's
+    string columns to its longest value)."""
+    OPS = importlib.import_module("inspektor-gadget_amd.operators")
+    E, H, G = igx.engine, igx.columns, igx.gadgets
+    Gk, n = 2000, 100_000
+    cdf = H.to_device(E.zipf_cdf(Gk, 1.1))
+    ev = E.gen_tcp(0xC2, 0, Gk, cdf, 0, n)
+    names = [k for k, _, _ in G.TopTcpTracer.EVENT]
+    tr = G.TopTcpTracer(MaxRows=60)
+    tr.feed({k: ev[k] for k in names})
+    direct = tr.NextEvent().Stats
+    tr.destroy()
+    mntns = sorted({s.MountNsID for s in direct})
+    prefix = "p" * 80
+    table = {m: ("node1", "ns", f"{prefix}-{(7 * j) % 5}-z", f"c{j}") for j, m in enumerate(mntns)}
+    desc = OPS.Get("top", "tcp")
+    parser = desc.Parser()
+    parser.SetFilters(["pod:~-[0-2]-z$"])
+    parser.SetSorting(["-pod", "-sent"])
+    got = []
+    parser.SetEventCallback(got.append)
+    ctx = OPS.GadgetContext("t2", desc, {"max-rows": 60, "events": lambda i: [{k: ev[k] for k in names}] if i < 1 else None},
+                            {"MountNsEnricher": {"containers": table}}, parser=parser)
+    assert OPS.LocalRuntime().RunGadget(ctx) is None
+    for s in direct:
+        s.Node, s.Namespace, s.Pod, s.Container = table[s.MountNsID]
+    keep = [s for s in direct if s.Pod[-3] in "012"]
+    pod = np.array([s.Pod.encode() for s in keep], dtype="S88").view(np.uint8).reshape(-1, 88)
+    sent = np.array([s.Sent for s in keep], np.uint64)
+    perm = oracle.go_sort_entries([(pod, "string", True), (sent, "uint64", True)], len(keep))
+    exp = [keep[int(i)] for i in perm]
+    assert 0 < len(got[0]) < len(direct)
+    assert [(s.FirstIndex, s.Pod) for s in got[0]] == [(s.FirstIndex, s.Pod) for s in exp]
