@@ -145,10 +145,10 @@ int igx_filter_parse(const igx_schema_col *cols, uint32_t ncols, const char *fil
 
 /* Regex rules (IGX_CMP_REGEX, on string columns) run on the device: the pattern is compiled
  * on the host to a DFA over rune classes with Go regexp semantics (RE2 syntax incl. \b \B
- * \A \z, (?m) (?i) (?s), \p{..} general categories, POSIX classes; UTF-8 decoded like
- * utf8.DecodeRune; unanchored MatchString).  Script classes (\p{Greek}) are not compiled:
- * igx_filter returns IGX_ENOTSUP.  igx_regex_compile_blob exposes the compiled automaton
- * (for tests and tools). */
+ * \A \z, (?m) (?i) (?s), \p{..} general categories and scripts of Unicode 13.0.0, POSIX
+ * classes; UTF-8 decoded like utf8.DecodeRune; unanchored MatchString).  A pattern whose
+ * automaton would exceed the device limits (255 rune classes, 2048 states) returns
+ * IGX_ENOTSUP.  igx_regex_compile_blob exposes the compiled automaton (for tests and tools). */
 int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *out, size_t cap,
                            size_t *out_len, char *errbuf, size_t errlen);
 

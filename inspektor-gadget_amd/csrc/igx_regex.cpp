@@ -7,9 +7,9 @@
 // `.` is any rune but '\n' (any rune with (?s)), `^`/`$` are the text's ends, or line ends
 // under (?m); \A \z \b \B are RE2's empty-width assertions (\b on ASCII word runes), \d \s
 // \w and the [[:name:]] classes are ASCII as in RE2, \pN / \p{Name} are Unicode general
-// categories (igx_unicode.h, Unicode 13.0.0 like Go 1.19), and (?i) folds every rune with its
-// simple-fold orbit (k ↔ K ↔ U+212A, s ↔ S ↔ U+017F, ...) -- classes too, as Go's parser
-// folds them.  Script names (\p{Greek}) are not compiled: IGX_ENOTSUP.  Syntax errors
+// categories or, after them, scripts (\p{Greek}; igx_unicode.h, Unicode 13.0.0 like Go 1.19),
+// and (?i) folds every rune with its simple-fold orbit (k ↔ K ↔ U+212A, s ↔ S ↔ U+017F, ...)
+// -- classes too, as Go's parser folds them (FoldCategory / FoldScript).  Syntax errors
 // surface at igx_filter_parse.
 //
 // Pipeline: recursive-descent parse -> Thompson NFA over rune sets and empty-width
@@ -116,6 +116,14 @@ bool unicode_class(const std::string &name, Ranges *out) {
             for (const auto &x : igx_unicode::kCatRanges)
                 if (x.cat == k) r.push_back({x.lo, x.hi});
         }
+    }
+    // unicode.Scripts, looked up after the categories and case-sensitively, as Go 1.19's
+    // regexp/syntax unicodeTable does; under (?i) group() adds the fold orbits (FoldScript)
+    for (int k = 0; !any && k < igx_unicode::kNumScripts; ++k) {
+        if (name != igx_unicode::kScripts[k]) continue;
+        any = true;
+        for (const auto &x : igx_unicode::kScriptRanges)
+            if (x.script == k) r.push_back({x.lo, x.hi});
     }
     if (!any) return false;
     *out = normalize(r);
@@ -247,9 +255,8 @@ struct Compiler {
             name = name.substr(1);
         }
         Ranges r;
-        if (!unicode_class(name, &r)) {
-            // a script name (\p{Greek}) or an unknown one: not compiled here
-            unsup = true;
+        if (!unicode_class(name, &r)) {   // neither a category nor a script: Go's ErrInvalidCharRange
+            err = "invalid character class range";
             return false;
         }
         *out = group(r, neg);

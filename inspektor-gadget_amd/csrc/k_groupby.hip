@@ -722,14 +722,24 @@ __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32
         if (gidx < first_ins) gmin(rec_first(a, gs), (unsigned long long)gidx);
         return;
     }
+    // A lane's entries are consecutive in the ring, so the server issues one slot's updates
+    // from adjacent lanes of one instruction: they fall in the slot's value record, one 64-B
+    // line, and leave the CU as one memory-side atomic request instead of one per update
+    // (top file: count and bytes of the same op, two updates per miss).
     bool has[NA + 1];
-    uint64_t mask[NA + 1];
-    uint32_t total = 0;
+    uint32_t c = 0;
 #pragma unroll
     for (int x = 0; x <= NA; ++x) {
         has[x] = x < NA ? (x < (int)a.naggs && v[x] != 0) : gidx < first_ins;
-        mask[x] = __ballot(has[x]);
-        total += (uint32_t)__popcll(mask[x]);
+        c += has[x] ? 1u : 0u;
+    }
+    const uint64_t lt = lanemask_lt();
+    uint32_t pre = 0, total = 0;   // wave prefix / total of c (c <= NA + 1 <= 5: three bits)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        const uint64_t m = __ballot((c >> b) & 1u);
+        pre += (uint32_t)__popcll(m & lt) << b;
+        total += (uint32_t)__popcll(m) << b;
     }
     if (!total) return;
     const uint64_t active = __ballot(true);
@@ -745,17 +755,15 @@ __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32
     }
     if ((a.dbg & 65536u) && spins && (threadIdx.x & 63) == leader)
         atomicAdd(a.dbg_cnt + 6, 1ull * spins);   // prober: update ring full
-    uint32_t off = base;
-    const uint64_t lt = lanemask_lt();
+    uint32_t p = base + pre;
 #pragma unroll
     for (int x = 0; x <= NA; ++x) {
         if (has[x]) {
-            const uint32_t p = off + (uint32_t)__popcll(mask[x] & lt);
             r.hi[p % ARING] = x < NA ? v[x] : gidx;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             r.lo[p % ARING] = make_uint2(gs, ring_lap(p) | (x < NA ? (uint32_t)x : WHAT_MIN));
+            ++p;
         }
-        off += (uint32_t)__popcll(mask[x]);
     }
 }
 

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 def _strings(n, seed=4):
     rng = np.random.default_rng(seed)
     words = [b"kworker/0:1", b"bash", b"sshd", b"containerd", b"Demo 123", b"demo", b"K8s-agent",
-             "café".encode(), b"\xff\xfebad", b"node_exporter", b"", b"x" * 16, b"a\nb"]
+             "café".encode(), b"\xff\xfebad", b"node_exporter", b"", b"x" * 16, b"a\nb",
+             "αβγ-api".encode(), "日本語ok".encode(), "µs".encode()]
     out = np.zeros((n, 16), np.uint8)
     pick = rng.integers(0, len(words), n)
     for i, k in enumerate(pick):
@@ -28,7 +29,9 @@ def _strings(n, seed=4):
                                   "~caf.", "~\\d+:\\d", "~^$", "~x{16}", "~(?s)a.b",
                                   # RE2 assertions, (?m), Unicode classes and folding
                                   "~\\bdemo\\b", "~\\Bsh", "~(?m)^b$", "~(?i)CAFÉ", "~\\p{Ll}{4}$",
-                                  "!~[[:upper:]]", "~\\pL\\PL"])
+                                  "!~[[:upper:]]", "~\\pL\\PL",
+                                  # Unicode 13.0.0 scripts (and FoldScript under (?i))
+                                  "~^\\p{Greek}", "~\\p{Han}{2}", "!~\\p{Latin}", "~(?i)^\\p{Greek}s$"])
 def test_regex_filter_on_device(oracle, igx, rule):
     H = igx.columns
     n = 100_003

@@ -122,8 +122,48 @@ def test_regex_errors_and_unsupported(igx):
     assert compile_blob(igx, rb"[\b]")[0] == igx._abi.IGX_EINVAL      # no \b inside a class in RE2
     assert compile_blob(igx, rb"\1")[0] == igx._abi.IGX_EINVAL        # backreferences do not exist
     assert compile_blob(igx, rb"[[:nope:]]")[0] == igx._abi.IGX_EINVAL
-    # script names need tables Python's unicodedata does not carry: not compiled
-    assert compile_blob(igx, rb"\p{Greek}")[0] == igx._abi.IGX_ENOTSUP
+    # neither a category nor a Unicode 13.0.0 script (names are case-sensitive in Go)
+    for bad in (rb"\p{Klingon}", rb"\p{greek}", rb"\p{Vithkuqi}", rb"\pQ", rb"[\p{Nope}a]"):
+        rc, msg = compile_blob(igx, bad)
+        assert rc == igx._abi.IGX_EINVAL and "invalid character class range" in msg, (bad, msg)
+
+
+# Unicode scripts (Go 1.19 unicode.Scripts, Unicode 13.0.0): cross-checked with the `regex`
+# module's \p{Script=..} on texts of runes that 13.0.0 assigns.  Under (?i) Go also adds
+# FoldScript (runes of other scripts whose fold orbit meets the script), which `regex` does
+# not: those are known answers below.
+SCRIPT_PATTERNS = [r"\p{Greek}", r"^\p{Greek}+$", r"\p{Han}", r"^\P{Latin}+$", r"\p{^Cyrillic}", r"^\p{Common}$",
+                   r"\p{Arabic}[0-9]", r"[\p{Hiragana}\p{Katakana}]+", r"^\p{Inherited}$", r"[^\p{Hangul}\s]",
+                   r"^[\p{Greek}\p{Latin}]+$"]
+SCRIPT_TEXTS = ["α", "Ω", "abc", "漢字", "ひらがなカタカナ", "Привет", "µ", "\u0345", "K", "\u212a", "ſ", "ﬀ",
+                "٣٤", "ب3", "한국어 ", "ǅ", "1", "", "αβγ1", "\u0300", "\u1f80", "ᾈ", "𐌰", "\U0001F600"]
+
+
+def _py_script(p):
+    import regex
+    return regex.compile(p.replace(r"\p{", r"\p{Script=").replace(r"\P{", r"\P{Script=")
+                         .replace(r"\p{Script=^", r"\P{Script=").replace("$", r"\Z"))
+
+
+@pytest.mark.parametrize("pattern", SCRIPT_PATTERNS)
+def test_regex_unicode_scripts(igx, pattern):
+    rc, blob = compile_blob(igx, pattern.encode())
+    assert rc == 0, blob
+    pr = _py_script(pattern)
+    for t in SCRIPT_TEXTS:
+        t = t.encode().decode("unicode_escape") if "\\" in t else t
+        assert run_blob(blob, t.encode()) == (pr.search(t) is not None), (pattern, t)
+
+
+def test_regex_script_fold_known_answers(igx):
+    r"""FoldScript: (?i)\p{Greek} takes the micro sign (Common) and U+0345 (Inherited), whose
+    orbits meet Greek; (?i)\p{Latin} takes the Kelvin sign's K (already Latin) and not Greek."""
+    ok = lambda p, t: run_blob(compile_blob(igx, p.encode())[1], t.encode())   # noqa: E731
+    assert ok(r"(?i)^\p{Greek}$", "\u00b5") and not ok(r"^\p{Greek}$", "\u00b5")
+    assert ok(r"(?i)^\p{Greek}$", "\u0345") and not ok(r"^\p{Greek}$", "\u0345")
+    assert not ok(r"(?i)^\p{Latin}$", "α") and ok(r"(?i)^\P{Greek}$", "a")
+    assert ok(r"(?i)^\p{Latin}$", "\u212a") and ok(r"(?i)^\p{Latin}+$", "ſK")      # both Latin already
+    assert ok(r"(?i)^\p{Greek}+$", "ΑΩω") and ok(r"(?i)^\p{Cyrillic}$", "\u1c80")  # ᲀ (Cyrillic) folds to в
 
 
 # Assertions and (?m): Python's re with re.ASCII has RE2's ASCII \b / \w and the same (?m)
