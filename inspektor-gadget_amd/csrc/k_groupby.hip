@@ -130,6 +130,7 @@ struct GbArgs {
     uint32_t krec_len;      // KR
     uint32_t krec_total;    // S x KR (< 2^32)
     uint32_t vrec_words;    // VR / 8
+    uint32_t vrec_total;    // S x VR when below 4 GiB (16-B buffer stores of a claim), else 0
     uint32_t *err;
     uint32_t *occ;          // occupancy bitmap, one bit per slot (set by the claimer)
     uint64_t ep;            // the interval's epoch (1..EP_MAX): tags and `ready` of older
@@ -332,11 +333,40 @@ __device__ __forceinline__ void probe_issue(const GbArgs &a, uint64_t h, uint32_
     load_rec<probe_quads<KW>()>(rec_rsrc(a), (uint32_t)(home_slot(a, h) * a.krec_len), d);
 }
 
-// d holds the home slot's record (probe_issue)
+// A claimer's value record: first = its event index, aggregate x = vinit[x] (the claiming
+// event's own values, so they need no atomic; null: 0), written through (sc1) as 16-B stores
+// where the record array allows buffer addressing -- a claim's stores are memory-side write
+// requests each, and they are the largest share of a high-cardinality interval's requests.
+// The padding words of the record are never read and not written.
+__device__ __forceinline__ void vrec_init(const GbArgs &a, uint64_t s, uint64_t gidx, const uint64_t *vinit) {
+    uint64_t *vr = a.vrec + s * a.vrec_words;
+    const uint32_t nw = 1 + a.naggs;
+    auto word = [&](uint32_t j) { return j == 0 ? gidx : (vinit ? vinit[j - 1] : 0ull); };
+    if (a.vrec_total) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.vrec, (short)0, (int)a.vrec_total, 0x00020000);
+        const uint32_t off = (uint32_t)(s * a.vrec_words * 8);
+        for (uint32_t j = 0; j < nw; j += 2) {
+            const uint64_t w0 = word(j), w1 = j + 1 < nw ? word(j + 1) : 0ull;
+            if (j + 1 < nw) {
+                const u4v q = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + 8 * j, 0, 16 /* sc1 */);
+            } else {
+                st_agent(vr + j, w0);
+            }
+        }
+    } else {
+        for (uint32_t j = 0; j < nw; ++j) st_agent(vr + j, word(j));
+    }
+}
+
+// d holds the home slot's record (probe_issue).  vinit (nullable): the event's aggregate values,
+// folded into the value record when this call claims the slot (claimed = true; the caller then
+// adds them nowhere else).
 template <int KW, bool SET_OCC = true>
 __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
                                                    uint64_t gidx, uint64_t &first_ins,
-                                                   uint32_t (&d)[probe_quads<KW>() * 4]) {
+                                                   uint32_t (&d)[probe_quads<KW>() * 4],
+                                                   const uint64_t *vinit = nullptr, bool *claimed = nullptr) {
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
     const uint64_t tag = (h & ~EP_MAX) | a.ep;
@@ -369,14 +399,14 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                         st_agent(reinterpret_cast<uint32_t *>(r + 4 * w), k[w]);
                     }
                 }
-                // the value record starts at first = first_ins, aggregates 0 (no reset pass)
-                uint64_t *vr = a.vrec + s * a.vrec_words;
-                st_agent(vr, gidx);
-                for (uint32_t x = 1; x < a.vrec_words; ++x) st_agent(vr + x, 0ull);
+                // the value record starts at first = first_ins and the claimer's own values
+                // (no reset pass)
+                vrec_init(a, s, gidx, vinit);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), (a.ep << 48) | (gidx + 1));
                 if (SET_OCC) atomicOr(a.occ + (s >> 5), 1u << (s & 31));
                 first_ins = gidx;
+                if (claimed) *claimed = vinit != nullptr;
                 return (uint32_t)s;
             }
             t = old;
@@ -900,8 +930,10 @@ __device__ __forceinline__ void read_cell(const MissRing<KW, NA> &m, uint32_t p,
 // (lost: PROBE)).
 template <int KW, int NA, bool DBG>
 __device__ __forceinline__ void finish_miss(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
-                                            const MissRow<KW, NA> &x, uint32_t gs, uint64_t first_ins) {
+                                            const MissRow<KW, NA> &x, uint32_t gs, uint64_t first_ins,
+                                            bool claimed = false) {
     const int ad = ghost_admit<KW>(a, c, x.h) ? lds_adopt<KW>(c, x.k, x.h, gs) : -1;
+    if (claimed) return;   // the claim wrote this event's values into the new record
     if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x.v, x.gidx);
     else ring_push<NA>(a, r, gs, x.v, x.gidx, first_ins);
 }
@@ -989,7 +1021,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
         if (st == PUB) {
             st_agent(reinterpret_cast<uint64_t *>(rec + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
             atomicOr(a.occ + (s >> 5), 1u << (s & 31));
-            finish_miss<KW, NA, DBG>(a, c, r, x, s, x.gidx);
+            finish_miss<KW, NA, DBG>(a, c, r, x, s, x.gidx, true);
             st = FREE;
         }
         // 5. claims: won -> write key and value record now, publish next iteration
@@ -1002,9 +1034,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
                     else
                         st_agent(reinterpret_cast<uint32_t *>(rec + 4 * w), x.k[w]);
                 }
-                uint64_t *vr = a.vrec + (uint64_t)s * a.vrec_words;
-                st_agent(vr, x.gidx);
-                for (uint32_t q = 1; q < a.vrec_words; ++q) st_agent(vr + q, 0ull);
+                vrec_init(a, s, x.gidx, x.v);   // with this event's own values (finish_miss skips them)
                 st = PUB;
             } else if (cas_old == tag) {
                 st = PROBE;   // lost to a claim of the same hash: read its key once `ready` is set
@@ -1109,10 +1139,12 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
             if (probe[j]) {
                 uint64_t first_ins = 0;
                 uint32_t gs;
+                bool claimed = false;
                 if (DBG && (a.dbg & 256u)) gs = (uint32_t)home_slot(a, x[j].h);   // diagnostics: no probe
-                else gs = find_or_insert<KW>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j]);
+                else gs = find_or_insert<KW>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j], x[j].v, &claimed);
                 if (gs != SLOT_OVF) {
                     const int ad = ghost_admit<KW>(a, c, x[j].h) ? lds_adopt<KW>(c, x[j].k, x[j].h, gs) : -1;
+                    if (claimed) continue;   // its values are in the new record already
                     if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x[j].v, x[j].gidx);
                     else ring_push<NA>(a, r, gs, x[j].v, x[j].gidx, first_ins);
                 }
@@ -1253,10 +1285,11 @@ __global__ __launch_bounds__(256) void k_groupby_direct(GbArgs a) {
             if (!ok[u]) continue;
             const uint64_t gidx = row_gidx(a, row0 + u * stride);
             uint64_t first_ins = 0;
+            bool claimed = false;
             // no occupancy bit: finalize rebuilds the bitmap from the tags (k_occ_from_tags),
             // one streaming pass instead of a memory-side atomic per claim
-            const uint32_t gs = find_or_insert<KW, false>(a, k[u], h[u], gidx, first_ins, d[u]);
-            if (gs == SLOT_OVF) continue;
+            const uint32_t gs = find_or_insert<KW, false>(a, k[u], h[u], gidx, first_ins, d[u], v[u], &claimed);
+            if (gs == SLOT_OVF || claimed) continue;
 #pragma unroll
             for (int x = 0; x < NA; ++x)
                 if (x < (int)a.naggs && v[u][x]) gadd(rec_agg(a, gs, x), (unsigned long long)v[u][x]);
@@ -2057,6 +2090,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.krec_len = t->krec_len;
     a.krec_total = (uint32_t)(t->nslots * t->krec_len);
     a.vrec_words = t->vrec_len / 8;
+    a.vrec_total = t->nslots * t->vrec_len < (1ull << 32) ? (uint32_t)(t->nslots * t->vrec_len) : 0u;
     a.err = t->err;
     a.occ = t->occ;
     a.ep = t->ep;

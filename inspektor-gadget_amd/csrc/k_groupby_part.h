@@ -573,8 +573,9 @@ __device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[K
     uint32_t d[probe_quads<KW>() * 4];
     probe_issue<KW>(a, h, d);
     uint64_t first_ins = 0;
-    const uint32_t gs = find_or_insert<KW, true>(a, k, h, first, first_ins, d);
-    if (gs == SLOT_OVF) return;
+    bool claimed = false;
+    const uint32_t gs = find_or_insert<KW, true>(a, k, h, first, first_ins, d, v, &claimed);
+    if (gs == SLOT_OVF || claimed) return;   // a claim wrote the values into the new record
 #pragma unroll
     for (int x = 0; x < NA; ++x)
         if (x < (int)a.naggs && v[x]) gadd(rec_agg(a, gs, x), (unsigned long long)v[x]);

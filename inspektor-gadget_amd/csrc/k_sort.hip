@@ -428,6 +428,182 @@ __global__ __launch_bounds__(TB) void k_sel_split(const uint32_t *__restrict__ W
     }
 }
 
+// ---- the same selection without host round trips ------------------------------------------
+// (top-K of keys without floats, where no NaN check is needed: the tables' SortStats).  The
+// first pass runs grid-wide with its bin picked on the device; the few candidates it leaves
+// (the rows of one 12-bit bin) are finished by one workgroup.
+struct SelState {
+    uint32_t bitpos, nbits, b, krem, n, acc_cnt, out_cnt, err;
+};
+
+__global__ void k_sel_init(const uint32_t *__restrict__ res, uint32_t nw, uint64_t n, uint32_t k, SelState *st) {
+    if (threadIdx.x) return;
+    uint32_t bitpos = nw * 32;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t diff = res[2 * w] ^ res[2 * w + 1];
+        if (diff) {
+            bitpos = 32 * w + (uint32_t)__clz(diff);
+            break;
+        }
+    }
+    st->bitpos = bitpos;
+    st->nbits = min((uint32_t)SEL_BITS, nw * 32 - min(bitpos, nw * 32));
+    st->b = 0;
+    st->krem = k;
+    st->n = (uint32_t)n;
+    st->acc_cnt = 0;
+    st->out_cnt = 0;
+    st->err = 0;
+}
+
+__global__ __launch_bounds__(TB) void k_sel_hist_d(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                   const SelState *__restrict__ st, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[SEL_BINS];
+    const uint32_t n = st->n, bitpos = st->bitpos, nbits = st->nbits;
+    if (n <= st->krem || nbits == 0) return;
+    for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB) h[b] = 0;
+    __syncthreads();
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < n; j += (uint64_t)gridDim.x * TB)
+        atomicAdd(&h[sel_digit(W, stride, nw, j, bitpos, nbits)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB)
+        if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// the bin holding the krem-th row: b, and the rows below it (accepted)
+__device__ __forceinline__ void sel_pick_block(const uint32_t *hist, uint32_t krem, uint32_t *tmp, uint32_t &b,
+                                               uint32_t &below, uint32_t &inb) {
+    // 1024 threads x 4 bins, inclusive prefix per thread, then across the block
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = hist[threadIdx.x * 4 + j];
+        s += v[j];
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan_1024(s, tmp, total);
+    uint32_t run = ex;
+    if (threadIdx.x == 0) tmp[16] = SEL_BINS;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (run < krem && run + v[j] >= krem) {   // exactly one bin crosses
+            tmp[16] = threadIdx.x * 4 + j;
+            tmp[17] = run;
+            tmp[18] = v[j];
+        }
+        run += v[j];
+    }
+    __syncthreads();
+    b = tmp[16];
+    below = tmp[17];
+    inb = tmp[18];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_sel_pick(const uint32_t *__restrict__ hist, SelState *st) {
+    __shared__ uint32_t tmp[20];
+    if (st->n <= st->krem || st->nbits == 0) return;
+    uint32_t b, below, inb;
+    sel_pick_block(hist, st->krem, tmp, b, below, inb);
+    if (threadIdx.x == 0) st->b = b;
+}
+
+// grid-wide split of pass 1 (rows are 0..n-1): digit < b -> acc, digit == b -> out
+__global__ __launch_bounds__(TB) void k_sel_split_d(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                    SelState *st, uint32_t *__restrict__ acc,
+                                                    uint32_t *__restrict__ out) {
+    const uint32_t n = st->n;
+    if (n <= st->krem || st->nbits == 0) return;
+    const uint32_t bitpos = st->bitpos, nbits = st->nbits, b = st->b;
+    __shared__ uint32_t lcnt[2], gbase[2];
+    if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t row[IPT], pos[IPT], kind[IPT];
+    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const uint64_t q = tbase + (uint64_t)j * TB + threadIdx.x;
+        kind[j] = 0;
+        row[j] = (uint32_t)q;
+        if (q < n) {
+            const uint32_t d = sel_digit(W, stride, nw, q, bitpos, nbits);
+            kind[j] = d < b ? 1u : (d == b ? 2u : 0u);
+        }
+        const uint64_t m1 = __ballot(kind[j] == 1), m2 = __ballot(kind[j] == 2);
+        uint32_t b1 = 0, b2 = 0;
+        if (lane == 0) {
+            if (m1) b1 = atomicAdd(&lcnt[0], (uint32_t)__popcll(m1));
+            if (m2) b2 = atomicAdd(&lcnt[1], (uint32_t)__popcll(m2));
+        }
+        b1 = __shfl(b1, 0);
+        b2 = __shfl(b2, 0);
+        pos[j] = kind[j] == 1 ? b1 + __popcll(m1 & lanemask_lt()) : b2 + __popcll(m2 & lanemask_lt());
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        gbase[0] = lcnt[0] ? atomicAdd(&st->acc_cnt, lcnt[0]) : 0;
+        gbase[1] = lcnt[1] ? atomicAdd(&st->out_cnt, lcnt[1]) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (kind[j] == 1) acc[gbase[0] + pos[j]] = row[j];
+        else if (kind[j] == 2) out[gbase[1] + pos[j]] = row[j];
+    }
+}
+
+// one workgroup: the remaining passes over the candidates of pass 1 (or all rows when n <= k),
+// then acc holds exactly k rows
+__global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
+                                                     SelState *st, uint32_t *__restrict__ acc, uint32_t *cnd0,
+                                                     uint32_t *cnd1) {
+    __shared__ uint32_t h[SEL_BINS];
+    __shared__ uint32_t tmp[20], cnt[2];
+    uint32_t n = st->n, krem = st->krem, bitpos = st->bitpos, nbits = st->nbits, nacc = 0;
+    const uint32_t *cand = nullptr;   // nullptr: rows 0..n-1
+    uint32_t *nxt = cnd0;
+    if (n > krem && nbits) {   // pass 1 ran grid-wide
+        nacc = st->acc_cnt;
+        krem -= nacc;
+        n = st->out_cnt;
+        cand = cnd0;
+        nxt = cnd1;
+        bitpos += nbits;
+    }
+    while (n > krem) {
+        if (bitpos >= nw * 32) {   // composed keys equal: cannot happen (the position is in them)
+            if (threadIdx.x == 0) st->err = 1;
+            return;
+        }
+        nbits = min((uint32_t)SEL_BITS, nw * 32 - bitpos);
+        for (uint32_t b = threadIdx.x; b < SEL_BINS; b += 1024) h[b] = 0;
+        if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < n; j += 1024)
+            atomicAdd(&h[sel_digit(W, stride, nw, cand ? cand[j] : j, bitpos, nbits)], 1u);
+        __syncthreads();
+        uint32_t b, below, inb;
+        sel_pick_block(h, krem, tmp, b, below, inb);
+        for (uint32_t j = threadIdx.x; j < n; j += 1024) {
+            const uint32_t i = cand ? cand[j] : j;
+            const uint32_t d = sel_digit(W, stride, nw, i, bitpos, nbits);
+            if (d < b) acc[nacc + atomicAdd(&cnt[0], 1u)] = i;
+            else if (d == b) nxt[atomicAdd(&cnt[1], 1u)] = i;
+        }
+        __syncthreads();
+        nacc += below;
+        krem -= below;
+        n = inb;
+        cand = nxt;
+        nxt = nxt == cnd0 ? cnd1 : cnd0;
+        bitpos += nbits;
+        __syncthreads();
+    }
+    for (uint32_t j = threadIdx.x; j < n; j += 1024) acc[nacc + j] = cand ? cand[j] : j;   // n == krem
+}
+
 // rank of acc[r] among the k accepted rows (full composed-key compare) -> out_perm
 __global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                  const uint32_t *__restrict__ acc, uint32_t k,
@@ -628,6 +804,8 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         KW += keys[k].words;
     }
     ca.rowmap = rowmap;
+    bool any_float = false;
+    for (uint32_t k = 0; k < nkeys; ++k) any_float = any_float || keys[k].kind == IGX_KIND_FLOAT;
     const uint32_t pos_words = (pos == nullptr) ? 1 : 2;
     KW += pos_words;
     if (KW > MAXW) return igx_fail(ctx, IGX_ENOTSUP, "sort: composed key too wide");
@@ -651,6 +829,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const size_t res_b = igx_align((size_t)KW * 8 + 4, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
+    static_assert(sizeof(SelState) <= 64 * 4, "SelState fits the 64 words before the selection histogram");
     void *s;
     int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b, &s);
     if (rc) return rc;
@@ -670,6 +849,27 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
     hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart);
     hipLaunchKernelGGL(k_andor_final, dim3(KW), dim3(TB), 0, ctx->stream, apart, ablocks, res);
+    if (use_sel && !any_float && rowmap) {
+        // top-K of a table's groups without host round trips (SelState on the device): no float
+        // key, so no NaN check; the first differing bit is found on the device; the position
+        // (first index) makes every composed key unique
+        uint32_t *acc = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b);
+        uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
+        SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
+        uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
+        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, ctx->stream, res, KW, nrows, limit, stp);
+        IGX_HIP(ctx, hipMemsetAsync(dh, 0, SEL_BINS * 4, ctx->stream));
+        const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, (nrows + TB - 1) / TB);
+        hipLaunchKernelGGL(k_sel_hist_d, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, stp, dh);
+        hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(1024), 0, ctx->stream, dh, stp);
+        hipLaunchKernelGGL(k_sel_split_d, dim3((uint32_t)((nrows + TILE - 1) / TILE)), dim3(TB), 0, ctx->stream, W[0],
+                           stride, KW, stp, acc, cnd[0]);
+        hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0], cnd[1]);
+        hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
+                           out_perm);
+        IGX_HIP(ctx, hipGetLastError());
+        return IGX_OK;
+    }
     uint32_t *hres;
     rc = igx_pinned(ctx, KW * 8 + 4, reinterpret_cast<void **>(&hres));
     if (rc) return rc;
