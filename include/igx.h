@@ -340,6 +340,14 @@ int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                   const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
                   uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
 
+/* The raw-key form of the same histograms: biolatency keys its map by hist_key{cmd_flags, dev}
+ * when targ_per_flag / targ_per_disk are set (biolatency.bpf.c:116-131), with any values.  Per
+ * event, slot[i] = min(log2l(delta[i] / divisor), nslots - 1) and keep[i] = delta[i] >= 0;
+ * a group-by with key (cmd_flags, dev, slot) and a COUNT of out_width 4 (the u32 slots) then
+ * holds every key's histogram (engine.hist_log2_keyed).  Asynchronous. */
+int igx_log2_slots(igx_ctx *ctx, const int64_t *delta, uint64_t nrows, uint64_t divisor, uint32_t nslots,
+                   uint8_t *slot, uint8_t *keep);
+
 /* ---- group:sum of float columns, IP text --------------------------------------------- */
 /* GroupEntries' float group:sum (group.go:133-156, flattenValues): perm (device u32, n) is a
  * stable sort of the rows by the group key (key_bytes at row * key_stride of keys); each run

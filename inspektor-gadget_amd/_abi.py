@@ -138,6 +138,7 @@ SIGNATURES = [
     ("igx_np_mark", _I, [_VP, _VP, _VP, _VP, _VP, _U64, _VP]),
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),
+    ("igx_log2_slots", _I, [_VP, _VP, _U64, _U64, _U32, _VP, _VP]),
     ("igx_partition_rows", _I, [_VP, _VP, _U64, _U32, _U32, _U32, _VP, _VP]),
     ("igx_dist_get_unique_id", _I, [_VP]),
     ("igx_dist_init", _I, [_VP, _VP, _I, _I, C.POINTER(_VP)]),

@@ -563,14 +563,18 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
     if (nrows == 0) return IGX_OK;                          // sort.go:36-38
     if (!out) return igx_fail(ctx, IGX_EINVAL, "sort: null output");
     std::vector<SortPlanKey> plan;
+    std::vector<GoSortKey> go;   // the same passes as sort.go runs them (the exact NaN path)
     uint32_t parity = 0;
     for (uint32_t i = 0; i < nkeys; ++i) {
         const igx_sortkey &k = keys[i];
         if (k.kind == IGX_KIND_BOOL || k.kind == IGX_KIND_OTHER) continue;   // sort.go:77-78
         if (k.width == 0) {   // constant column: a pass that orders nothing, parity only
             parity ^= k.desc ? 1u : 0u;
+            go.push_back(GoSortKey{nullptr, 0, k.kind, 0, k.desc ? 0u : 1u, 1u});
             continue;
         }
+        go.push_back(GoSortKey{static_cast<const uint8_t *>(k.ptr), k.width, k.kind, strides ? strides[i] : k.width,
+                               k.desc ? 0u : 1u, 0u});
         SortPlanKey p{};
         p.ptr = static_cast<const uint8_t *>(k.ptr);
         p.width = k.width;
@@ -597,7 +601,7 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
         return launch_sort_perm(ctx, nullptr, 0, nrows, nullptr, false, nullptr, out, limit, rowmap);
     }
     return launch_sort_perm(ctx, plan.data(), (uint32_t)plan.size(), nrows, pos, parity != 0, valid, out, limit,
-                            rowmap, pos_stride);
+                            rowmap, pos_stride, go.data(), (uint32_t)go.size());
 }
 
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
@@ -625,6 +629,12 @@ extern "C" int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, u
                         const uint64_t *pos, uint32_t k, uint32_t *out_idx) {
     if (k == 0) return IGX_OK;
     return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, nullptr, out_idx, k, nullptr);
+}
+
+extern "C" int igx_log2_slots(igx_ctx *ctx, const int64_t *delta, uint64_t nrows, uint64_t divisor, uint32_t nslots,
+                              uint8_t *slot, uint8_t *keep) {
+    if (!ctx) return IGX_EINVAL;
+    return launch_log2_slots(ctx, delta, nrows, divisor, nslots, slot, keep);
 }
 
 extern "C" int igx_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, const int64_t *delta,

@@ -81,12 +81,25 @@ struct SortPlanKey {
 // IP text of n rows (rowmap nullable) -> out, n x IGX_IPTEXT_WIDTH bytes (k_sort.hip)
 int launch_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t astride, const uint8_t *fam, uint32_t fstride,
                    const uint32_t *rowmap, uint64_t n, uint8_t *out);
+// One sort pass as sort.go runs it (raw sortBy order and direction), for the exact SliceStable
+// path (k_gostable.hip) that a NaN in a float key needs.
+struct GoSortKey {
+    const uint8_t *ptr;
+    uint32_t width, kind, stride;
+    uint32_t asc;     // no '-' prefix (columns.OrderAsc)
+    uint32_t konst;   // constant column (no data): a pass that compares every row equal
+};
 // rowmap (device, nullable): row r reads its keys / pos at rowmap[r] and the permutation
-// reports rowmap[r] (used to sort a table's groups through its slot list).
+// reports rowmap[r] (used to sort a table's groups through its slot list).  gokeys (nullable):
+// every pass in sortBy order, for the exact path when a float key holds a NaN (without them that
+// case returns IGX_ENOTSUP).
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap,
-                     uint32_t pos_stride = 8);
+                     uint32_t pos_stride = 8, const GoSortKey *gokeys = nullptr, uint32_t ngokeys = 0);
+// data (device, n rows in the pre-sort order) sorted in place by Go 1.19 SliceStable, pass by pass
+int launch_go_stable(igx_ctx *ctx, const GoSortKey *keys, uint32_t nkeys, uint64_t nrows, const uint8_t *valid,
+                     uint32_t *data);
 // closed-form planning + launch (igx_host.cpp); strides per key (nullable = widths)
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
@@ -95,3 +108,5 @@ int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *stri
 int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                      const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,
                      uint32_t ncont, uint64_t divisor, uint32_t nslots, uint32_t *hist);
+int launch_log2_slots(igx_ctx *ctx, const int64_t *delta, uint64_t n, uint64_t divisor, uint32_t nslots,
+                      uint8_t *slot, uint8_t *keep);

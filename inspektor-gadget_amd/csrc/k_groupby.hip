@@ -338,35 +338,44 @@ __device__ __forceinline__ void probe_issue(const GbArgs &a, uint64_t h, uint32_
 // where the record array allows buffer addressing -- a claim's stores are memory-side write
 // requests each, and they are the largest share of a high-cardinality interval's requests.
 // The padding words of the record are never read and not written.
-__device__ __forceinline__ void vrec_init(const GbArgs &a, uint64_t s, uint64_t gidx, const uint64_t *vinit) {
+// (All indices are compile-time: a register array indexed at run time would live in scratch.)
+template <int NV>
+__device__ __forceinline__ void vrec_init(const GbArgs &a, uint64_t s, uint64_t gidx, const uint64_t (&v)[NV]) {
+    uint64_t w[NV + 2];
+    w[0] = gidx;
+#pragma unroll
+    for (int x = 0; x < NV; ++x) w[1 + x] = v[x];
+    w[NV + 1] = 0;
     uint64_t *vr = a.vrec + s * a.vrec_words;
-    const uint32_t nw = 1 + a.naggs;
-    auto word = [&](uint32_t j) { return j == 0 ? gidx : (vinit ? vinit[j - 1] : 0ull); };
+    const uint32_t nw = 1 + a.naggs;   // <= 1 + NV
     if (a.vrec_total) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.vrec, (short)0, (int)a.vrec_total, 0x00020000);
         const uint32_t off = (uint32_t)(s * a.vrec_words * 8);
-        for (uint32_t j = 0; j < nw; j += 2) {
-            const uint64_t w0 = word(j), w1 = j + 1 < nw ? word(j + 1) : 0ull;
-            if (j + 1 < nw) {
-                const u4v q = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+#pragma unroll
+        for (int j = 0; j < NV + 1; j += 2) {
+            if ((uint32_t)j >= nw) break;
+            if ((uint32_t)j + 1 < nw) {
+                const u4v q = {(uint32_t)w[j], (uint32_t)(w[j] >> 32), (uint32_t)w[j + 1], (uint32_t)(w[j + 1] >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b128(q, rs, off + 8 * j, 0, 16 /* sc1 */);
             } else {
-                st_agent(vr + j, w0);
+                st_agent(vr + j, w[j]);
             }
         }
     } else {
-        for (uint32_t j = 0; j < nw; ++j) st_agent(vr + j, word(j));
+#pragma unroll
+        for (int j = 0; j < NV + 1; ++j)
+            if ((uint32_t)j < nw) st_agent(vr + j, w[j]);
     }
 }
 
-// d holds the home slot's record (probe_issue).  vinit (nullable): the event's aggregate values,
-// folded into the value record when this call claims the slot (claimed = true; the caller then
-// adds them nowhere else).
-template <int KW, bool SET_OCC = true>
+// d holds the home slot's record (probe_issue).  vinit: the event's aggregate values, written
+// into the value record when this call claims the slot (claimed = true; the caller then adds
+// them nowhere else).
+template <int KW, bool SET_OCC, int NV>
 __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
                                                    uint64_t gidx, uint64_t &first_ins,
                                                    uint32_t (&d)[probe_quads<KW>() * 4],
-                                                   const uint64_t *vinit = nullptr, bool *claimed = nullptr) {
+                                                   const uint64_t (&vinit)[NV], bool &claimed) {
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
     const uint64_t tag = (h & ~EP_MAX) | a.ep;
@@ -401,12 +410,12 @@ __device__ __forceinline__ uint32_t find_or_insert(const GbArgs &a, const uint32
                 }
                 // the value record starts at first = first_ins and the claimer's own values
                 // (no reset pass)
-                vrec_init(a, s, gidx, vinit);
+                vrec_init<NV>(a, s, gidx, vinit);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_agent(reinterpret_cast<uint64_t *>(r + KOFF + 8), (a.ep << 48) | (gidx + 1));
                 if (SET_OCC) atomicOr(a.occ + (s >> 5), 1u << (s & 31));
                 first_ins = gidx;
-                if (claimed) *claimed = vinit != nullptr;
+                claimed = true;
                 return (uint32_t)s;
             }
             t = old;
@@ -1034,7 +1043,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
                     else
                         st_agent(reinterpret_cast<uint32_t *>(rec + 4 * w), x.k[w]);
                 }
-                vrec_init(a, s, x.gidx, x.v);   // with this event's own values (finish_miss skips them)
+                vrec_init<NA>(a, s, x.gidx, x.v);   // with this event's own values (finish_miss skips them)
                 st = PUB;
             } else if (cas_old == tag) {
                 st = PROBE;   // lost to a claim of the same hash: read its key once `ready` is set
@@ -1141,7 +1150,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                 uint32_t gs;
                 bool claimed = false;
                 if (DBG && (a.dbg & 256u)) gs = (uint32_t)home_slot(a, x[j].h);   // diagnostics: no probe
-                else gs = find_or_insert<KW>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j], x[j].v, &claimed);
+                else gs = find_or_insert<KW, true, NA>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j], x[j].v, claimed);
                 if (gs != SLOT_OVF) {
                     const int ad = ghost_admit<KW>(a, c, x[j].h) ? lds_adopt<KW>(c, x[j].k, x[j].h, gs) : -1;
                     if (claimed) continue;   // its values are in the new record already
@@ -1288,7 +1297,7 @@ __global__ __launch_bounds__(256) void k_groupby_direct(GbArgs a) {
             bool claimed = false;
             // no occupancy bit: finalize rebuilds the bitmap from the tags (k_occ_from_tags),
             // one streaming pass instead of a memory-side atomic per claim
-            const uint32_t gs = find_or_insert<KW, false>(a, k[u], h[u], gidx, first_ins, d[u], v[u], &claimed);
+            const uint32_t gs = find_or_insert<KW, false, NA>(a, k[u], h[u], gidx, first_ins, d[u], v[u], claimed);
             if (gs == SLOT_OVF || claimed) continue;
 #pragma unroll
             for (int x = 0; x < NA; ++x)

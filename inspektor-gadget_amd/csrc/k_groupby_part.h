@@ -574,7 +574,7 @@ __device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[K
     probe_issue<KW>(a, h, d);
     uint64_t first_ins = 0;
     bool claimed = false;
-    const uint32_t gs = find_or_insert<KW, true>(a, k, h, first, first_ins, d, v, &claimed);
+    const uint32_t gs = find_or_insert<KW, true, NA>(a, k, h, first, first_ins, d, v, claimed);
     if (gs == SLOT_OVF || claimed) return;   // a claim wrote the values into the new record
 #pragma unroll
     for (int x = 0; x < NA; ++x)

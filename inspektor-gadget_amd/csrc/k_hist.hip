@@ -239,6 +239,18 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
     }
 }
 
+// ig_profio_done's slot per event for the raw hist_key{cmd_flags, dev} form (biolatency.bpf.c:
+// 116-150): slot = min(log2l(delta / divisor), nslots - 1), kept iff delta >= 0 (:113-114).
+__global__ __launch_bounds__(256) void k_log2_slots(const int64_t *__restrict__ delta, uint64_t n, uint64_t divisor,
+                                                    uint32_t nslots, uint8_t *__restrict__ slot,
+                                                    uint8_t *__restrict__ keep) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const int64_t d = delta[i];
+        keep[i] = d >= 0;
+        slot[i] = d >= 0 ? (uint8_t)slot_of<0>(d, divisor, nslots) : 0;
+    }
+}
+
 template <int DIV>
 void launch(const HistArgs &a, uint32_t blocks, size_t lds, hipStream_t s, bool vec) {
     static bool attr_set = false;
@@ -311,6 +323,17 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
     else if (divisor == 1000000) launch<1000000>(a, blocks, lds, ctx->stream, use_vec);
     else if (divisor == 1) launch<1>(a, blocks, lds, ctx->stream, use_vec);
     else launch<0>(a, blocks, lds, ctx->stream, use_vec);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
+
+int launch_log2_slots(igx_ctx *ctx, const int64_t *delta, uint64_t n, uint64_t divisor, uint32_t nslots,
+                      uint8_t *slot, uint8_t *keep) {
+    if (n == 0) return IGX_OK;
+    if (!delta || !slot || !keep) return igx_fail(ctx, IGX_EINVAL, "log2_slots: null argument");
+    if (nslots == 0 || nslots > 64 || divisor == 0) return igx_fail(ctx, IGX_EINVAL, "log2_slots: bad nslots/divisor");
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)ctx->num_cus * 16);
+    hipLaunchKernelGGL(k_log2_slots, dim3(blocks), dim3(256), 0, ctx->stream, delta, n, divisor, nslots, slot, keep);
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }

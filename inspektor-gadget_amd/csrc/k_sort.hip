@@ -785,9 +785,40 @@ int launch_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t astride, const ui
     return IGX_OK;
 }
 
+// The pre-sort order when there is no position column: row r (or rowmap[r])
+__global__ void k_iota_map(uint32_t *out, const uint32_t *rowmap, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = rowmap ? rowmap[i] : (uint32_t)i;
+}
+
+// A NaN in a float key: run SliceStable itself (k_gostable.hip) from the pre-sort order.
+static int sort_exact_go(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows, const uint64_t *pos,
+                         const uint8_t *valid, uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap,
+                         uint32_t pos_stride, const GoSortKey *gokeys, uint32_t ngokeys) {
+    for (uint32_t k = 0; k < nkeys; ++k)
+        if (keys[k].direct)   // per-row rendered text (IP addresses) is indexed by sorted row, not by source row
+            return igx_fail(ctx, IGX_ENOTSUP, "sort: NaN float key together with an IP-text key");
+    uint32_t *data = nullptr;
+    IGX_HIP(ctx, hipMalloc(&data, nrows * 4));
+    int rc = IGX_OK;
+    if (pos)   // rows in position order (a sort on the position alone)
+        rc = launch_sort_perm(ctx, nullptr, 0, nrows, pos, false, nullptr, data, 0, rowmap, pos_stride);
+    else
+        hipLaunchKernelGGL(k_iota_map, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, ctx->stream, data, rowmap,
+                           nrows);
+    if (!rc) rc = launch_go_stable(ctx, gokeys, ngokeys, nrows, valid, data);
+    const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+    if (!rc && hipMemcpyAsync(out_perm, data, m * 4, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess) rc = IGX_EIO;
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(data);
+    if (rc) return rc == IGX_EIO ? igx_fail(ctx, rc, "sort: exact path copy failed") : rc;
+    return IGX_OK;
+}
+
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
-                     uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride) {
+                     uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride,
+                     const GoSortKey *gokeys, uint32_t ngokeys) {
     if (nrows == 0) return IGX_OK;
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
     if (nkeys > NSK) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than %d keys", NSK);
@@ -877,10 +908,12 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     // Go's `<` is unordered on NaN, so getLessFunc (sort.go:125-135) is no strict weak order
     // once a NaN is present and SliceStable's result depends on its insertion-sort blocks and
-    // symMerge steps, not on the values alone: no radix order reproduces it.
-    if (hres[2 * KW])
-        return igx_fail(ctx, IGX_ENOTSUP, "sort: NaN in a float sort key (Go's SliceStable order under an "
-                                          "unordered comparison is not reproduced)");
+    // symMerge steps, not on the values alone: no radix order reproduces it, so the passes run
+    // as SliceStable itself (k_gostable.hip).
+    if (hres[2 * KW]) {
+        if (!gokeys) return igx_fail(ctx, IGX_ENOTSUP, "sort: NaN in a float sort key");
+        return sort_exact_go(ctx, keys, nkeys, nrows, pos, valid, out_perm, limit, rowmap, pos_stride, gokeys, ngokeys);
+    }
 
     if (use_sel) {
         // top-K: radix select on the composed keys, then rank the k survivors

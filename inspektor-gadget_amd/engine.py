@@ -334,6 +334,52 @@ def hist_log2(dev, cont, delta, devs, ncont, divisor=1000, nslots=27, hist=None)
     return hist
 
 
+def hist_log2_keyed(delta, cmd_flags=None, dev=None, divisor=1000, nslots=27, capacity=1 << 16):
+    """biolatency with targ_per_flag / targ_per_disk (biolatency.bpf.c:116-150): one log2
+    histogram per distinct raw hist_key{cmd_flags, dev}, any values (a column left None is the
+    key field the BPF program leaves 0).  igx_log2_slots gives each event its slot, then a
+    group-by on (cmd_flags, dev, slot) counts them (u32 slots, wrapping like the BPF map's).
+    Returns [(cmd_flags, dev, u32 slots (nslots,))] in the order of each key's first event (the
+    BPF map's own order is its hash order)."""
+    import numpy as np
+    from .columns import host
+    torch = torch_mod()
+    ctx = context()
+    n = delta.numel()
+    slot = torch.empty(max(4, (n + 3) // 4 * 4), dtype=torch.uint8, device=delta.device)[:n]
+    keep = torch.empty(max(4, (n + 3) // 4 * 4), dtype=torch.uint8, device=delta.device)[:n]
+    if n:
+        ctx.check(ctx.L.igx_log2_slots(ctx.h, ptr(delta), n, divisor, nslots, ptr(slot), ptr(keep)))
+    cols, widths = [], []
+    for c in (cmd_flags, dev):
+        if c is not None:
+            cols.append(c)
+            widths.append(4)
+    cols.append(slot)
+    widths.append(1)
+    tab = Table(widths, [Agg(_abi.AGG_COUNT, 0, _abi.NO_COL, 4, 0)], capacity)
+    try:
+        if n:
+            tab.update(cols, list(range(len(cols))), n, valid=keep)
+        fin = tab.finalize()
+        keys, aggs, first = table_tensors(tab, fin)
+    finally:
+        tab.destroy()
+    k, cnt, f = host(keys), host(aggs[0]), host(first)
+    nk = len(widths) - 1
+    w = k[:, :4 * nk].copy().view(np.uint32).reshape(len(k), nk) if nk else np.zeros((len(k), 0), np.uint32)
+    sl = k[:, 4 * nk]
+    out = {}
+    for i in range(len(k)):
+        vals = [int(x) for x in w[i]]
+        cf = vals.pop(0) if cmd_flags is not None else 0
+        dv = vals.pop(0) if dev is not None else 0
+        e = out.setdefault((cf, dv), [np.zeros(nslots, np.uint32), int(f[i])])
+        e[0][sl[i]] = np.uint32(int(cnt[i]) & 0xFFFFFFFF)
+        e[1] = min(e[1], int(f[i]))
+    return [(cf, dv, h) for (cf, dv), (h, _) in sorted(out.items(), key=lambda kv: kv[1][1])]
+
+
 # ------------------------------------------------------------------------------------
 # data movement either side of the path
 # ------------------------------------------------------------------------------------

@@ -731,26 +731,46 @@ class ProfileBlockIOTracer:
     every I/O); devs=[MKDEV(major, minor), ...] (and ncont > 1 with a container column)
     keys per device (and per container), the C3 extension.  ms=True is targ_ms."""
 
-    def __init__(self, devs=None, ncont=1, ms=False):
+    def __init__(self, devs=None, ncont=1, ms=False, per_disk=False, per_flag=False):
         self.devs = list(devs or [])
         self.ncont = ncont
         self.divisor = 1000000 if ms else 1000
         self.val_type = "msecs" if ms else "usecs"
         self.hist = None
+        # targ_per_disk / targ_per_flag (biolatency.bpf.c:116-131): histograms keyed by the raw
+        # hist_key{cmd_flags, dev} values instead of the dense dev x container index
+        self.per_disk, self.per_flag = per_disk, per_flag
+        self.keyed = {}   # (cmd_flags, dev) -> u32 slots, in first-event order
 
-    def feed(self, delta_ns, dev=None, cont=None):
+    def feed(self, delta_ns, dev=None, cont=None, cmd_flags=None):
+        if self.per_disk or self.per_flag:
+            import numpy as np
+            for cf, dv, h in engine.hist_log2_keyed(delta_ns, cmd_flags if self.per_flag else None,
+                                                    dev if self.per_disk else None, self.divisor, MAX_SLOTS):
+                cur = self.keyed.setdefault((cf, dv), np.zeros(MAX_SLOTS, np.uint32))
+                cur += h   # u32 wrap, like __sync_fetch_and_add on the map's u32 slots
+            return
         self.hist = engine.hist_log2(dev, cont, delta_ns, self.devs, self.ncont, self.divisor,
                                      MAX_SLOTS, hist=self.hist)
 
     def slots(self):
-        """u32 slots per key, host numpy (nkeys, 27)."""
+        """u32 slots per key, host numpy (nkeys, 27); keyed mode: in first-event order."""
         import numpy as np
+        if self.per_disk or self.per_flag:
+            if not self.keyed:
+                return np.zeros((0, MAX_SLOTS), np.uint32)
+            return np.stack(list(self.keyed.values()))
         if self.hist is None:
             return np.zeros((max(1, len(self.devs)) * self.ncont, MAX_SLOTS), np.uint32)
         return host(self.hist)
 
+    def keys(self):
+        """keyed mode: the hist_key{cmd_flags, dev} of each row of slots()."""
+        return list(self.keyed.keys())
+
     def getReport(self, key: int = 0) -> Report:
-        """The reference reads the first key only (NextKey(nil)); key picks one here."""
+        """The reference reads the first key only (NextKey(nil), the BPF map's hash order); key
+        picks one here (first-event order in keyed mode)."""
         return getReport(self.slots()[key], self.val_type)
 
     def Stop(self) -> str:

@@ -439,3 +439,38 @@ def test_streaming_intervals_double_buffered(oracle, igx, torch, G):
     st2 = G.StreamingTopTracer(G.TopTcpTracer, Iterations=2, MaxRows=5, capacity=2 * Gk)
     assert len(list(st2.run(intervals))) == 2
     st2.destroy()
+
+
+def test_profile_block_io_raw_keys(oracle, igx, torch):
+    """targ_per_disk / targ_per_flag (biolatency.bpf.c:116-131): one histogram per raw
+    hist_key{cmd_flags, dev} (any values, including 0 and 0xffffffff), counts equal to the
+    oracle's per-key log2 histograms; negative deltas skipped (:113-114); two feeds accumulate;
+    keys in first-event order."""
+    E, H, G = igx.engine, igx.columns, igx.gadgets
+    rng = np.random.default_rng(5)
+    n = 400_000
+    q = E.lognormal_quantiles(np.log(2e5), 1.5)
+    ev = E.gen_bio(0xC3, H.to_device(q), 0, 2 * n)
+    delta = H.host(ev["delta"].view(torch.int64)).copy()
+    delta[rng.integers(0, 2 * n, 1000)] = -5
+    flags_pool = np.array([0, 1, 0x801, 0x4001, 0xFFFFFFFF], np.uint32)
+    devs_pool = np.array([(8 << 20) | 0, (8 << 20) | 16, (259 << 20) | 1, 0], np.uint32)
+    cf = flags_pool[rng.integers(0, len(flags_pool), 2 * n)]
+    dv = devs_pool[rng.integers(0, len(devs_pool), 2 * n)]
+    for per_disk, per_flag in ((True, False), (False, True), (True, True)):
+        tr = G.ProfileBlockIOTracer(per_disk=per_disk, per_flag=per_flag)
+        for b in range(2):
+            sl = slice(b * n, (b + 1) * n)
+            tr.feed(H.to_device(delta[sl]), dev=H.to_device(dv[sl]), cmd_flags=H.to_device(cf[sl]))
+        kf = cf if per_flag else np.zeros(2 * n, np.uint32)
+        kd = dv if per_disk else np.zeros(2 * n, np.uint32)
+        order = []   # keys by their first kept event (a negative delta never creates a key)
+        for a, b, d in zip(kf.tolist(), kd.tolist(), delta.tolist()):
+            if d >= 0 and (a, b) not in order:
+                order.append((a, b))
+        got_keys = tr.keys()
+        assert got_keys == order
+        for key, h in zip(got_keys, tr.slots()):
+            m = (kf == key[0]) & (kd == key[1])
+            ref = oracle.hist_log2(None, None, delta[m], [], 1)[0]
+            assert np.array_equal(h, ref), key

@@ -238,3 +238,27 @@ def test_get_report_quirk(oracle):
     rep = O.get_report(slots)
     assert len(rep) == 7 and rep[3]["count"] == 5 and rep[3]["intervalStart"] == 8
     assert O.get_report([4] + [0] * 26) == []
+
+
+@pytest.mark.parametrize("trial", range(3))
+def test_go_stable_with_nan_c_matches_py(oracle, trial):
+    """NaN float keys (getLessFunc's `<` unordered, sort.go:125-135): the order is whatever
+    Go 1.19's SliceStable does; the C restatement (the GPU NaN path's checker) equals the
+    pure-Python transliteration of stable_func on random inputs with NaNs, nil rows, several
+    keys and both directions (n up to 300: insertion blocks and several merge levels)."""
+    O = oracle
+    rng = random.Random(77 + trial)
+    for _ in range(40):
+        n = rng.randint(0, 300)
+        nk = rng.randint(1, 3)
+        vals = [[rng.choice([float("nan"), -1.0, 0.0, 2.5, 3.0, float("inf")]) for _ in range(n)] for _ in range(nk)]
+        descs = [rng.random() < 0.5 for _ in range(nk)]
+        valid = [rng.random() > 0.1 for _ in range(n)]
+        rows = [r if valid[r] else None for r in range(n)]
+        py = O.go_sort_entries_py(rows, [(lambda r, v=v: v[r], d) for v, d in zip(vals, descs)])
+        py = [r if r is not None else None for r in py]
+        cperm = O.go_sort_entries([(np.array(v, np.float64), "float64", d) for v, d in zip(vals, descs)], n,
+                                  valid=np.array(valid, np.uint8))
+        # nil rows come back as None from the py version, in order of their row ids
+        nil_rows = iter([r for r in cperm if not valid[r]])
+        assert [r if r is not None else next(nil_rows) for r in py] == list(cperm)

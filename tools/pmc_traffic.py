@@ -40,6 +40,8 @@ def main():
     p.add_argument("--anchor", default=None,
                    help="a chain of kernels per update (the partitioned form): sum every --kernel match "
                         "and divide by the launches of this one")
+    p.add_argument("--extra", action="append", default=[],
+                   help="another kernel of the same step whose per-launch traffic is added (e.g. k_np_mark)")
     p.add_argument("--config", required=True)
     p.add_argument("--out", required=True)
     a = p.parse_args()
@@ -51,7 +53,11 @@ def main():
         nw = len(_values(a.write, "WRITE_SIZE", a.anchor))
     fetch_b = 2.0 * 1024.0 * sum(f) / nf
     write_b = 1024.0 * sum(w) / nw
-    out = {"kernel": a.kernel, "config": json.loads(a.config),
+    for k in a.extra:
+        ef, ew = _values(a.fetch, "FETCH_SIZE", k), _values(a.write, "WRITE_SIZE", k)
+        fetch_b += 2.0 * 1024.0 * sum(ef) / len(ef)
+        write_b += 1024.0 * sum(ew) / len(ew)
+    out = {"kernel": a.kernel, "extra": a.extra, "config": json.loads(a.config),
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "traffic_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
            "anchor": a.anchor,
