@@ -212,16 +212,17 @@ def run_c2(a, ctx):
         clk.on = record
         with clk:
             tab.update(cols, list(range(8)), N, base, preds)
-        fin = tab.finalize()                          # syncs: group count for the top-K
-        # SortStats(["-sent","-recv"]) over the table's groups, first K slots
+        tab.finalize(sync=False)                      # the group count stays on the device
+        # SortStats(["-sent","-recv"]) over the table's groups, first K slots (the device top-K
+        # reads the count there: the step has no host round trip)
         cand = tab.gather(tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K))
         if world > 1:
             cand = D.merge_topk(cand, 72, 2, [(0, True), (1, True)], K)
-        st["cand"], st["G"] = cand, fin["n_groups"]
+        st["cand"] = cand
 
     torch.cuda.synchronize()
     dt = T.run(step, a.steps, a.warmup)
-    Gn = st["G"]
+    Gn = tab.wait()                                   # the last interval's group count
     alg = N * EV_BYTES + Gn * GROUP_BYTES
     out = {"value": world * N * a.steps / dt, "ms_per_step": dt * 1000.0 / a.steps, "groups_per_gpu": Gn,
            "roofline": roofline(alg, clk.avg(), "k_groupby<ip_key_t>",
@@ -376,23 +377,24 @@ def run_c4(a, ctx):
         with clk:   # the bracket holds every kernel that reads the 24 B/event: np_mark and the update
             keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
             tab.update(cols, [0, 1, 2, 3], n, rank * n, valid=keep)
-        fin = tab.finalize()
         if world > 1:
+            fin = tab.finalize()
             rows = table_rows(E, torch, tab, fin)
             mine = D.exchange_rows(rows, fin["key_bytes"])
             D.merge_partials(mine, widths, [], cap, table=own)
-            fin = own.fin
-        st["G"] = fin["n_groups"]
+            st["G"] = own.fin["n_groups"]
+        else:
+            tab.finalize(sync=False)                  # the distinct count is read after the loop
 
     dt = T.run(step, a.config_steps, 1)
     ms = dt * 1000.0 / a.config_steps
-    ng = st["G"]
+    ng = st["G"] if world > 1 else tab.wait()
     alg = n * 24 + ng * 20
     out = {"workload": "advise network-policy: np_mark + distinct (src, dir, peer, port) with first index"
                        + (", partial groups all-to-all by key owner + owner merge" if world > 1 else ""),
            "events_per_gpu": n, "value": world * n / (ms * 1e-3), "unit": "events/s", "ms_per_step": ms,
            "distinct_on_rank0": ng,
-           "roofline": roofline(n * 24 + st["G"] * 20, clk.avg(),
+           "roofline": roofline(n * 24 + ng * 20, clk.avg(),
                                 "k_np_mark + igx_groupby_update on the np tuple (AUTO: the partitioned form's "
                                 "passes k_gbp_count/csum/scan/offs/a/b/c after the first, measured, interval)",
                                 "24 B/event (src 4, peer 4, port 2, pkt 1, type 1, proto 1, hostip 4, raddr 4, "
@@ -454,20 +456,23 @@ def run_c5(a, ctx):
         clk.on = record
         with clk:
             tab.update(cols, [0, 1, 2, 3], n, rank * n)
-        fin = tab.finalize()
         t = tab
         if world > 1:
+            fin = tab.finalize()
+            st["G"] = fin["n_groups"]
             rows = table_rows(E, torch, tab, fin)
             mine = D.exchange_rows(rows, fin["key_bytes"])
             t = D.merge_partials(mine, widths, [8, 8, 8, 8], cap, table=own)
+        else:
+            tab.finalize(sync=False)                  # the top-K reads the group count on the device
         cand = t.gather(t.sort([(A.TSRC_AGG, 3, True)], K))       # ["-wbytes"]
         if world > 1:
             cand = D.merge_topk(cand, 20, 4, [(3, True)], K)
-        st["G"], st["cand"] = fin["n_groups"], cand
+        st["cand"] = cand
 
     dt = T.run(step, a.config_steps, 1)
     ms = dt * 1000.0 / a.config_steps
-    ng = st["G"]
+    ng = st["G"] if world > 1 else tab.wait()
     alg = n * 25 + ng * 60
     out = {"workload": "top file: group-by (inode, dev, pid, tid) with reads/rbytes/writes/wbytes, top-20 by "
                        "[-wbytes]" + (", partial groups all-to-all by key owner, owners' top-20 all-gathered"

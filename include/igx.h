@@ -290,6 +290,19 @@ int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t ncols,
                           uint64_t base_idx);
 /* Synchronises; fills the view; IGX_ENOSPC if capacity was exceeded. */
 int igx_groupby_finalize(igx_table *t, igx_table_view *view);
+/* igx_groupby_finalize without its host synchronisation: the occupied-slot list is built on
+ * the device and the group count stays there (view->d_n_groups; view->n_groups is 0 until
+ * igx_groupby_wait).  igx_groupby_sort's top-K of such a table (0 < k <= 4096, no float or
+ * IP-text key) reads the count on the device, so a whole interval -- reset, update,
+ * finalize, sort, gather -- is issued without a host round trip (nextStats' drain,
+ * tracer.go:177-226, with no wait in it).  The count and the status igx_groupby_finalize
+ * would have returned (IGX_ENOSPC) come back from igx_groupby_wait, or from the first
+ * igx_groupby_reset / igx_groupby_finalize that finds the read-back landed (a reset never
+ * waits for the device).  Asynchronous. */
+int igx_groupby_finalize_async(igx_table *t, igx_table_view *view);
+/* Waits for the last igx_groupby_finalize_async: *n_groups (nullable) = its group count;
+ * returns its status.  IGX_OK (and the last known count) when none is pending. */
+int igx_groupby_wait(igx_table *t, uint64_t *n_groups);
 /* Materialise groups idx[0..k) (device u32, e.g. igx_topk output) as packed rows of
  * key_bytes | naggs x u64 | first_idx u64 into out_rows (device) -- the Stats rows
  * nextStats builds (pkg/gadgets/top/tcp/tracer/tracer.go:186-219).  Call after

@@ -127,6 +127,8 @@ SIGNATURES = [
     ("igx_groupby_update_ex", _I, [_VP, C.POINTER(Col), _U32, C.POINTER(_U32), C.POINTER(Pred),
                                    _U32, _VP, _U32, _U64, _U64]),
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
+    ("igx_groupby_finalize_async", _I, [_VP, C.POINTER(TableView)]),
+    ("igx_groupby_wait", _I, [_VP, C.POINTER(C.c_uint64)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
     ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
     ("igx_segment_fsum", _I, [_VP, _VP, _U32, _U32, _VP, _U64, _VP, _VP, _U32, _VP]),

@@ -92,18 +92,21 @@ struct GoSortKey {
 // rowmap (device, nullable): row r reads its keys / pos at rowmap[r] and the permutation
 // reports rowmap[r] (used to sort a table's groups through its slot list).  gokeys (nullable):
 // every pass in sortBy order, for the exact path when a float key holds a NaN (without them that
-// case returns IGX_ENOTSUP).
+// case returns IGX_ENOTSUP).  d_nrows (device, nullable): the row count lives on the device and
+// nrows is only its upper bound -- top-K without a float key or nil mask only (the device
+// selection); out_perm entries past the count are 0xFFFFFFFF.
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap,
-                     uint32_t pos_stride = 8, const GoSortKey *gokeys = nullptr, uint32_t ngokeys = 0);
+                     uint32_t pos_stride = 8, const GoSortKey *gokeys = nullptr, uint32_t ngokeys = 0,
+                     const uint64_t *d_nrows = nullptr);
 // data (device, n rows in the pre-sort order) sorted in place by Go 1.19 SliceStable, pass by pass
 int launch_go_stable(igx_ctx *ctx, const GoSortKey *keys, uint32_t nkeys, uint64_t nrows, const uint8_t *valid,
                      uint32_t *data);
 // closed-form planning + launch (igx_host.cpp); strides per key (nullable = widths)
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
-                     uint32_t limit, uint32_t *out, uint32_t direct_mask = 0);
+                     uint32_t limit, uint32_t *out, uint32_t direct_mask = 0, const uint64_t *d_nrows = nullptr);
 
 int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                      const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,

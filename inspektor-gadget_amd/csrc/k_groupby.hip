@@ -1475,6 +1475,10 @@ struct igx_table {
     uint8_t *p_mask = nullptr;   // row mask of the predicates that are not fused (grow-only)
     size_t p_mask_bytes = 0;
     uint64_t host_groups = 0;
+    uint64_t *fin_host = nullptr;   // pinned: group count, error word, LDS misses (finalize read-back)
+    hipEvent_t fin_ev = nullptr;    // recorded after an asynchronous finalize's read-back copies
+    bool fin_pending = false;       // igx_groupby_finalize_async not yet collected
+    int fin_status = 0;             // status of a collected asynchronous finalize, not yet returned
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[32] = {};      // IP text of the groups, per IGX_TSRC_IPTEXT sort key
     uint64_t text_rows[32] = {};
@@ -1581,6 +1585,8 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMalloc(&t->occ, t->occ_words * 4);
     if (e == hipSuccess) e = hipMalloc(&t->n_groups, 64);
     if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&t->fin_host), 32, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fin_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream);
     if (e != hipSuccess) {
         igx_groupby_destroy(t);
@@ -1590,9 +1596,18 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     return igx_groupby_reset(t);
 }
 
+static int fin_collect(igx_table *t, uint64_t *n_groups);
+
 extern "C" int igx_groupby_reset(igx_table *t) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
+    // an asynchronous finalize whose read-back has landed is collected now (its AUTO
+    // bookkeeping then steers this interval); one still in flight is collected by a later
+    // call, so a reset never waits for the device.  A collected error is returned after the
+    // reset is done.
+    if (t->fin_pending && hipEventQuery(t->fin_ev) == hipSuccess) (void)fin_collect(t, nullptr);
+    const int pending_rc = t->fin_status;
+    t->fin_status = IGX_OK;
     // A new interval is a new epoch: records of older epochs read as empty and a claimer
     // initialises its value record, so only the bitmap and the error word are cleared.
     if (++t->ep > EP_MAX) {
@@ -1605,7 +1620,7 @@ extern "C" int igx_groupby_reset(igx_table *t) {
     IGX_HIP(ctx, hipMemsetAsync(t->err, 0, 16, ctx->stream));   // error bits + LDS-miss count
     t->rows_fed = 0;
     t->host_groups = 0;
-    return IGX_OK;
+    return pending_rc;
 }
 
 extern "C" int igx_groupby_destroy(igx_table *t) {
@@ -1623,6 +1638,8 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->p_cnt);
     (void)hipFree(t->p_mask);
     for (auto *p : t->text) (void)hipFree(p);
+    if (t->fin_host) (void)hipHostFree(t->fin_host);
+    if (t->fin_ev) (void)hipEventDestroy(t->fin_ev);
     delete t;
     return IGX_OK;
 }
@@ -2167,8 +2184,9 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     return IGX_OK;
 }
 
-extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
-    if (!t) return IGX_EINVAL;
+// finalize's device part: the occupied-slot list and the group count, then the count, the
+// error word and the LDS-miss count copied to the table's pinned read-back buffer
+static int fin_launch(igx_table *t) {
     igx_ctx *ctx = t->ctx;
     const uint64_t tiles = (t->nslots + CT - 1) / CT;
     if (t->interval_direct)
@@ -2180,14 +2198,33 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
     hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                        t->tile_cnt, t->groups);
     IGX_HIP(ctx, hipGetLastError());
-    uint64_t *h;
-    int rc = igx_pinned(ctx, 24, reinterpret_cast<void **>(&h));
-    if (rc) return rc;
-    IGX_HIP(ctx, hipMemcpyAsync(h, t->n_groups, 8, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipMemcpyAsync(h + 1, t->err, 16, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(t->fin_host, t->n_groups, 8, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(t->fin_host + 1, t->err, 16, hipMemcpyDeviceToHost, ctx->stream));
+    return IGX_OK;
+}
+
+static void fin_view(igx_table *t, igx_table_view *view, uint64_t ng) {
+    if (!view) return;
+    view->n_groups = ng;
+    view->n_slots = t->nslots;
+    view->key_bytes = t->key_words * 4;
+    view->key_stride = t->krec_len;
+    view->val_stride = t->vrec_len;
+    view->naggs = t->naggs;
+    view->keys = t->krec;
+    for (uint32_t x = 0; x < 16; ++x) view->aggs[x] = x < t->naggs ? t->vrec + 1 + x : nullptr;
+    view->first_idx = t->vrec;
+    view->groups = t->groups;
+    view->d_n_groups = t->n_groups;
+}
+
+// finalize's host part, once the read-back has landed: the count, the AUTO bookkeeping and
+// the interval's status
+static int fin_apply(igx_table *t) {
+    igx_ctx *ctx = t->ctx;
+    const uint64_t *h = t->fin_host;
     const uint64_t ng = h[0];
-    const uint32_t err = reinterpret_cast<uint32_t *>(h)[2];
+    const uint32_t err = reinterpret_cast<const uint32_t *>(h)[2];
     const uint64_t misses = h[2];
     t->host_groups = ng;
     // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
@@ -2199,24 +2236,57 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
         t->prefer_sm = misses * 10 > t->rows_fed * 7;
         if (t->mode == IGX_GB_AUTO && misses * 100 > t->rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }
-    if (view) {
-        view->n_groups = ng;
-        view->n_slots = t->nslots;
-        view->key_bytes = t->key_words * 4;
-        view->key_stride = t->krec_len;
-        view->val_stride = t->vrec_len;
-        view->naggs = t->naggs;
-        view->keys = t->krec;
-        for (uint32_t x = 0; x < 16; ++x) view->aggs[x] = x < t->naggs ? t->vrec + 1 + x : nullptr;
-        view->first_idx = t->vrec;
-        view->groups = t->groups;
-        view->d_n_groups = t->n_groups;
-    }
     if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
     if (ng > t->cap)
         return igx_fail(ctx, IGX_ENOSPC, "groupby: %llu distinct keys exceed capacity %llu",
                         (unsigned long long)ng, (unsigned long long)t->cap);
     return IGX_OK;
+}
+
+// waits for a pending asynchronous finalize and applies it; its status is kept in fin_status
+// until a call returns it (igx_groupby_wait, reset, finalize)
+static int fin_collect(igx_table *t, uint64_t *n_groups) {
+    if (t->fin_pending) {
+        t->fin_pending = false;
+        IGX_HIP(t->ctx, hipEventSynchronize(t->fin_ev));
+        const int rc = fin_apply(t);
+        if (rc && !t->fin_status) t->fin_status = rc;
+    }
+    if (n_groups) *n_groups = t->host_groups;
+    return t->fin_status;
+}
+
+extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
+    if (!t) return IGX_EINVAL;
+    igx_ctx *ctx = t->ctx;
+    (void)fin_collect(t, nullptr);   // the read-back buffer is about to be reused
+    int rc = fin_launch(t);
+    if (rc) return rc;
+    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    rc = fin_apply(t);
+    fin_view(t, view, t->host_groups);
+    if (!rc) rc = t->fin_status;     // an earlier asynchronous finalize's error is not lost
+    t->fin_status = IGX_OK;
+    return rc;
+}
+
+extern "C" int igx_groupby_finalize_async(igx_table *t, igx_table_view *view) {
+    if (!t) return IGX_EINVAL;
+    igx_ctx *ctx = t->ctx;
+    (void)fin_collect(t, nullptr);   // the previous one landed long ago (it precedes this interval)
+    const int rc = fin_launch(t);
+    if (rc) return rc;
+    IGX_HIP(ctx, hipEventRecord(t->fin_ev, ctx->stream));
+    t->fin_pending = true;
+    fin_view(t, view, 0);
+    return IGX_OK;
+}
+
+extern "C" int igx_groupby_wait(igx_table *t, uint64_t *n_groups) {
+    if (!t) return IGX_EINVAL;
+    const int rc = fin_collect(t, n_groups);
+    t->fin_status = IGX_OK;
+    return rc;
 }
 
 extern "C" int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows) {
@@ -2244,6 +2314,25 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
     if (nkeys > 32) return igx_fail(ctx, IGX_ENOTSUP, "groupby_sort: more than 32 keys");
+    // After an asynchronous finalize the group count is on the device: a top-K whose keys the
+    // device selection handles (no float, no IP text) runs over at most min(capacity, slots)
+    // rows bounded by that count; anything else waits for the count first.
+    const uint64_t *d_count = nullptr;
+    uint64_t nrows = t->host_groups;
+    if (t->fin_pending) {
+        bool dev_ok = k > 0 && k <= 4096 && 2ull * k < std::min<uint64_t>(t->cap, t->nslots);
+        for (uint32_t i = 0; i < nkeys && dev_ok; ++i) {
+            const igx_tsortkey &q = keys[i];
+            if (q.src == IGX_TSRC_IPTEXT || (q.src == IGX_TSRC_KEY && q.kind == IGX_KIND_FLOAT)) dev_ok = false;
+        }
+        if (dev_ok) {
+            d_count = t->n_groups;
+            nrows = std::min<uint64_t>(t->cap, t->nslots);
+        } else {
+            (void)fin_collect(t, nullptr);   // its status stays for igx_groupby_wait / the next reset
+            nrows = t->host_groups;
+        }
+    }
     igx_sortkey sk[32];
     uint32_t strides[32];
     uint32_t direct = 0;
@@ -2297,8 +2386,8 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
             return igx_fail(ctx, IGX_EINVAL, "groupby_sort: bad source");
         }
     }
-    return sort_common_rows(ctx, sk, strides, nkeys, t->host_groups, t->groups,
-                            t->vrec, t->vrec_len, k, out_slots, direct);
+    return sort_common_rows(ctx, sk, strides, nkeys, nrows, t->groups, t->vrec, t->vrec_len, k, out_slots, direct,
+                            d_count);
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.

@@ -37,6 +37,7 @@ struct ComposeArgs {
     const uint64_t *pos;
     const uint8_t *valid;
     const uint32_t *rowmap;
+    const uint64_t *d_n;  // nullable: the row count on the device (n is then its upper bound)
     uint64_t n, stride;   // stride = words array pitch (elements)
     uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN
 };
@@ -54,7 +55,7 @@ __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, ui
 __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
                                                 uint32_t *__restrict__ payload) {
     uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= a.n) return;
+    if (i >= a.n || (a.d_n && i >= *a.d_n)) return;
     const uint64_t src = a.rowmap ? a.rowmap[i] : i;   // where row i's values live
     bool nil = a.valid && a.valid[src] == 0;
     uint32_t w = 0;
@@ -115,8 +116,10 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
 // 16-byte loads, four in flight per lane; partials, not atomics: the words' results share
 // one line, and same-line atomics from every workgroup serialise at the memory side.
 __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words, uint64_t n,
-                                              uint64_t stride, uint32_t *__restrict__ part) {
+                                              uint64_t stride, uint32_t *__restrict__ part,
+                                              const uint64_t *__restrict__ d_n) {
     __shared__ uint32_t red[2][TB / 64];
+    if (d_n) n = min(n, *d_n);
     const uint32_t w = blockIdx.y;
     const uint32_t *col = words + (uint64_t)w * stride;   // stride is a multiple of 64 rows
     const uint4 *v4 = reinterpret_cast<const uint4 *>(col);
@@ -436,8 +439,10 @@ struct SelState {
     uint32_t bitpos, nbits, b, krem, n, acc_cnt, out_cnt, err;
 };
 
-__global__ void k_sel_init(const uint32_t *__restrict__ res, uint32_t nw, uint64_t n, uint32_t k, SelState *st) {
+__global__ void k_sel_init(const uint32_t *__restrict__ res, uint32_t nw, uint64_t n, uint32_t k, SelState *st,
+                           const uint64_t *__restrict__ d_n) {
     if (threadIdx.x) return;
+    if (d_n) n = min(n, *d_n);
     uint32_t bitpos = nw * 32;
     for (uint32_t w = 0; w < nw; ++w) {
         const uint32_t diff = res[2 * w] ^ res[2 * w + 1];
@@ -607,9 +612,17 @@ __global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict_
 // rank of acc[r] among the k accepted rows (full composed-key compare) -> out_perm
 __global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                  const uint32_t *__restrict__ acc, uint32_t k,
-                                                 const uint32_t *__restrict__ payload, uint32_t *__restrict__ out) {
+                                                 const uint32_t *__restrict__ payload, uint32_t *__restrict__ out,
+                                                 const SelState *__restrict__ st) {
     __shared__ uint32_t red[TB / 64];
     const uint32_t r = blockIdx.x;
+    if (st) {   // the row count was on the device: fewer rows than k leave the tail unset
+        k = min(k, st->n);
+        if (r >= k) {
+            if (threadIdx.x == 0) out[r] = 0xFFFFFFFFu;
+            return;
+        }
+    }
     const uint32_t me = acc[r];
     uint32_t less = 0;
     for (uint32_t j = threadIdx.x; j < k; j += TB) {
@@ -818,7 +831,7 @@ static int sort_exact_go(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, 
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride,
-                     const GoSortKey *gokeys, uint32_t ngokeys) {
+                     const GoSortKey *gokeys, uint32_t ngokeys, const uint64_t *d_nrows) {
     if (nrows == 0) return IGX_OK;
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
     if (nkeys > NSK) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than %d keys", NSK);
@@ -835,6 +848,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         KW += keys[k].words;
     }
     ca.rowmap = rowmap;
+    ca.d_n = d_nrows;
     bool any_float = false;
     for (uint32_t k = 0; k < nkeys; ++k) any_float = any_float || keys[k].kind == IGX_KIND_FLOAT;
     const uint32_t pos_words = (pos == nullptr) ? 1 : 2;
@@ -859,6 +873,8 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     constexpr uint32_t ANDOR_BLOCKS = 256;
     const size_t res_b = igx_align((size_t)KW * 8 + 4, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
+    if (d_nrows && !(use_sel && !any_float && rowmap && !valid))   // only the device selection reads the count there
+        return igx_fail(ctx, IGX_EINVAL, "sort: a device row count needs a top-K without float keys or nil mask");
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     static_assert(sizeof(SelState) <= 64 * 4, "SelState fits the 64 words before the selection histogram");
     void *s;
@@ -878,7 +894,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
     const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
     uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
-    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart);
+    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
     hipLaunchKernelGGL(k_andor_final, dim3(KW), dim3(TB), 0, ctx->stream, apart, ablocks, res);
     if (use_sel && !any_float && rowmap) {
         // top-K of a table's groups without host round trips (SelState on the device): no float
@@ -888,7 +904,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
         SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
         uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
-        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, ctx->stream, res, KW, nrows, limit, stp);
+        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, ctx->stream, res, KW, nrows, limit, stp, d_nrows);
         IGX_HIP(ctx, hipMemsetAsync(dh, 0, SEL_BINS * 4, ctx->stream));
         const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, (nrows + TB - 1) / TB);
         hipLaunchKernelGGL(k_sel_hist_d, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, stp, dh);
@@ -897,7 +913,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                            stride, KW, stp, acc, cnd[0]);
         hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0], cnd[1]);
         hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
-                           out_perm);
+                           out_perm, stp);
         IGX_HIP(ctx, hipGetLastError());
         return IGX_OK;
     }
@@ -967,7 +983,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             IGX_HIP(ctx, hipMemcpyAsync(acc + (limit - krem), cand, (size_t)krem * 4, hipMemcpyDeviceToDevice,
                                         ctx->stream));
         hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
-                           out_perm);
+                           out_perm, nullptr);
         IGX_HIP(ctx, hipGetLastError());
         return IGX_OK;
     }

@@ -223,6 +223,15 @@ class Table:
                                               ptr(valid), _abi.NO_COL if idx_col is None else idx_col,
                                               n, base_idx))
 
+    def wait(self):
+        """igx_groupby_wait: the group count of the last finalize(sync=False), with its status
+        (IGX_ENOSPC raises as finalize would have)."""
+        n = C.c_uint64()
+        self.ctx.check(self.ctx.L.igx_groupby_wait(self.h, C.byref(n)))
+        if getattr(self, "fin", None) is not None:
+            self.fin["n_groups"] = n.value
+        return n.value
+
     def reset(self):
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
 
@@ -230,12 +239,17 @@ class Table:
         """igx_groupby_set_mode: _abi.GB_AUTO (default), GB_CACHED, GB_DIRECT or GB_PART."""
         self.ctx.check(self.ctx.L.igx_groupby_set_mode(self.h, mode))
 
-    def finalize(self):
-        """Synchronises.  Returns the table view (raw device pointers, slot-indexed) as a
-        dict; `groups_ptr` lists the n_groups occupied slots."""
+    def finalize(self, sync=True):
+        """Returns the table view (raw device pointers, slot-indexed) as a dict; `groups_ptr`
+        lists the n_groups occupied slots.  sync=True synchronises (igx_groupby_finalize);
+        sync=False leaves the group count on the device (igx_groupby_finalize_async:
+        n_groups is None until wait(), and a top-K sort reads the count on the device)."""
         v = TableView()
-        self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
-        self.fin = {"n_groups": v.n_groups, "n_slots": v.n_slots, "key_bytes": v.key_bytes,
+        if sync:
+            self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
+        else:
+            self.ctx.check(self.ctx.L.igx_groupby_finalize_async(self.h, C.byref(v)))
+        self.fin = {"n_groups": v.n_groups if sync else None, "n_slots": v.n_slots, "key_bytes": v.key_bytes,
                     "key_stride": v.key_stride, "val_stride": v.val_stride, "keys_ptr": v.keys,
                     "aggs_ptr": [v.aggs[i] for i in range(v.naggs)], "first_ptr": v.first_idx,
                     "groups_ptr": v.groups, "d_n_groups": v.d_n_groups}
@@ -257,7 +271,14 @@ class Table:
                 ts.append(_abi.TSortKey(src, int(what or 0), 0, 0, 0, int(desc)))
         arr = (_abi.TSortKey * max(1, len(ts)))(*ts)
         G = self.fin["n_groups"]
-        m = G if k == 0 else min(k, G)
+        if G is None:   # finalize(sync=False): a top-K over integer keys reads the count on the device
+            dev_ok = 0 < k <= 4096 and 2 * k < self.capacity and all(t.src != _abi.TSRC_IPTEXT and not (t.src == _abi.TSRC_KEY and
+                                                                             t.kind == _abi.KIND_FLOAT) for t in ts)
+            if not dev_ok:
+                G = self.wait()
+        # without the count, k slots come back; those past the group count are 0xFFFFFFFF
+        # (gather() turns them into zero rows)
+        m = k if G is None else (G if k == 0 else min(k, G))
         out = torch.empty(max(1, m), dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
         if m:
             self.ctx.check(self.ctx.L.igx_groupby_sort(self.h, arr, len(ts), m, ptr(out)))

@@ -259,6 +259,61 @@ def test_table_sort_and_gather(oracle, E, H, igx, torch):
     tab.destroy()
 
 
+def test_async_finalize_device_count_topk(oracle, E, H, igx, torch):
+    """igx_groupby_finalize_async: no host round trip in the interval; the top-K (integer
+    keys) reads the group count on the device and equals the synchronous path's, over several
+    intervals; fewer groups than k leave 0xFFFFFFFF slots (zero rows from gather); the count
+    and a capacity overflow come back from igx_groupby_wait."""
+    A = igx._abi
+    G, n = 8000, 400_000
+    ev_h = oracle.gen_tcp(0xC2, 0, G, oracle.zipf_cdf(G, 1.1), 0, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    names = ("pid", "lport", "family")
+    aggs = [A.Agg(A.AGG_SUM, 3, A.NO_COL, 8, 0), A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)]
+    cols = [ev[k] for k in names] + [ev["size"]]
+    tab = E.Table([4, 2, 2], aggs, 2 * G)
+    keys = [(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, False)]
+    want = []
+    for it in range(3):   # the synchronous path, three intervals of growing size
+        tab.reset()
+        m = n // (3 - it)
+        tab.update(cols, [0, 1, 2], m, 0)
+        g = tab.finalize()["n_groups"]
+        want.append((g, H.host(tab.gather(tab.sort(keys, 20)))))
+    for it in range(3):
+        tab.reset()
+        m = n // (3 - it)
+        tab.update(cols, [0, 1, 2], m, 0)
+        fin = tab.finalize(sync=False)
+        assert fin["n_groups"] is None
+        got = H.host(tab.gather(tab.sort(keys, 20)))
+        assert tab.wait() == want[it][0]
+        assert np.array_equal(got, want[it][1])
+    # fewer groups than k
+    tab.reset()
+    tab.update([c[:12] for c in cols], [0, 1, 2], 12, 0)
+    tab.finalize()
+    g_few = tab.fin["n_groups"]
+    ref = H.host(tab.gather(tab.sort(keys, 20)))
+    tab.reset()
+    tab.update([c[:12] for c in cols], [0, 1, 2], 12, 0)
+    tab.finalize(sync=False)
+    slots = tab.sort(keys, 20)
+    rows = H.host(tab.gather(slots))
+    assert tab.wait() == g_few < 20
+    assert np.array_equal(rows[:g_few], ref[:g_few])
+    assert (H.host(slots)[g_few:].view(np.uint32) == 0xFFFFFFFF).all() and not rows[g_few:].any()
+    tab.destroy()
+    # capacity overflow: reported by wait(), not by finalize(sync=False)
+    small = E.Table([4], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], 1000)
+    small.update([ev["pid"]], [0], n, 0)
+    small.finalize(sync=False)
+    with pytest.raises(A.IgxError) as ei:
+        small.wait()
+    assert ei.value.code == A.IGX_ENOSPC
+    small.destroy()
+
+
 def test_netpolicy_mark_and_masked_distinct(oracle, E, H, igx, torch):
     """igx_np_mark (advisor.go:279-292) + distinct over the kept rows (valid mask)."""
     A = igx._abi
