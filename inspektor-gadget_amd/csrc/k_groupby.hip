@@ -1716,9 +1716,11 @@ static int grow(igx_ctx *ctx, void **p, size_t *have, size_t need) {
     return IGX_OK;
 }
 
-// The partitioned form (k_groupby_part.h): passes K, O, S, A, B, C.
+// The partitioned form (k_groupby_part.h): passes K, O, S, A, B, C -- or, in the region
+// variant (AUTO's miss-heavy intervals), A, T, B, I, C: no count pass, buckets filled through
+// cursors into regions of 1.25x their share of the rows.
 template <class L, int NV>
-static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
+static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bool region) {
     constexpr int KW = L::KW;
     constexpr uint32_t TRA = PTA * part_rows<KW, NV>();
     if (4 * p.rq > (uint32_t)part_w<KW, NV>()) return igx_fail(ctx, IGX_EINVAL, "groupby_update: record layout");
@@ -1761,13 +1763,37 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     p.nchunk = (p.tiles_a + CHT - 1) / CHT;
     const uint64_t tiles_b = a.n / trb + F1 + 1;
     const uint64_t items_max = NB + a.n / p.ch + 1;
+    uint64_t r1 = a.n * 5 / 4 / F1 + TRA, r2 = a.n * 5 / 4 / NB + 1024;   // region records
+    if (const char *d = std::getenv("IGX_GBP_REGSIZE"))   // tests: small regions overflow
+        r1 = r2 = std::max<uint64_t>(1, std::strtoull(d, nullptr, 0));
+    if (region && (r1 * F1 >= (1ull << 31) || r2 * NB >= (1ull << 31))) region = false;
+    if (region) {
+        p.reg1 = (uint32_t)r1;
+        p.reg2 = (uint32_t)r2;
+        // scratch: rc1 | rc2 | tstart | bt | istart | itfb | ctl (u32 words)
+        const uint64_t words = F1 + NB + (F1 + 1) + tiles_b + (NB + 1) + items_max + 4;
+        int rc = grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
+        if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes,
+                           (size_t)16 * p.rq * (r1 * F1 + r2 * NB));
+        if (rc) return rc;
+        p.rc1 = t->p_cnt;
+        p.rc2 = p.rc1 + F1;
+        p.tstart = p.rc2 + NB;
+        p.bt = p.tstart + F1 + 1;
+        p.istart = p.bt + tiles_b;
+        p.itfb = p.istart + NB + 1;
+        p.ctl = p.itfb + items_max;
+        p.recs1 = t->p_recs;
+        p.recs2 = t->p_recs + r1 * F1 * p.rq * 4;
+    }
     // scratch: cnt1 | csum | hist | start2 | cur2 | tstart | bt | istart | itfb | ctl (u32 words)
     const uint64_t w_cnt1 = (uint64_t)p.tiles_a * F1, w_csum = (uint64_t)p.nchunk * F1;
     const uint64_t words = w_cnt1 + w_csum + NB + (NB + 1) + NB + (F1 + 1) + tiles_b + (NB + 1) + items_max + 4;
-    int rc = grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
+    int rc = region ? IGX_OK : grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
     const size_t rec_bytes = (size_t)16 * p.rq;
-    if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes, 2 * rec_bytes * a.n);
+    if (!rc && !region) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes, 2 * rec_bytes * a.n);
     if (rc) return rc;
+    if (!region) {
     p.cnt1 = t->p_cnt;
     p.csum = p.cnt1 + w_cnt1;
     p.hist = p.csum + w_csum;
@@ -1780,6 +1806,7 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     p.ctl = p.itfb + items_max;
     p.recs1 = t->p_recs;
     p.recs2 = t->p_recs + (uint64_t)a.n * p.rq * 4;
+    }
     const size_t lds_k = 4 * ((size_t)NB + F1);
     const size_t lds_a = (size_t)TRA * (16 * p.rq + 1) + 12 * (size_t)F1 + 4 * 17;
     const size_t lds_b = (size_t)trb * (16 * p.rq + 6) + 12 * (size_t)F2 + 4 * 17;
@@ -1799,6 +1826,16 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
         }
     }
     const uint32_t cus = (uint32_t)ctx->num_cus;
+    if (region) {
+        IGX_HIP(ctx, hipMemsetAsync(p.rc1, 0, 4ull * (F1 + NB), ctx->stream));
+        hipLaunchKernelGGL((k_gbp_a<L, NV>), dim3(p.tiles_a), dim3(PTA), lds_a, ctx->stream, a, p);
+        if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
+        hipLaunchKernelGGL(k_gbr_tiles, dim3(1), dim3(1024), 0, ctx->stream, p);
+        hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
+        if (p.dbg & 512u) return IGX_OK;   // ... after pass B
+        hipLaunchKernelGGL(k_gbr_items, dim3(1), dim3(1024), 0, ctx->stream, p);
+    }
+    if (!region) {
     IGX_HIP(ctx, hipMemsetAsync(p.hist, 0, 4ull * NB, ctx->stream));
     hipLaunchKernelGGL((k_gbp_count<L, NV>), dim3(std::min<uint32_t>(p.tiles_a, 2 * cus)), dim3(PTA), lds_k,
                        ctx->stream, a, p);
@@ -1810,6 +1847,7 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p) {
     if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
     hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
     if (p.dbg & 512u) return IGX_OK;   // ... after pass B
+    }
     if (t->naggs)
         hipLaunchKernelGGL((k_gbp_c<KW, NV, AMAX>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     else   // distinct-only (C4): no aggregate decode or accumulate in the per-record path
@@ -1894,9 +1932,12 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
         a.validw = 1;
         a.npred = 0;
     }
-    if (nv == 0) return launch_part_as<L, 0>(t, ctx, a, p);
-    if (nv <= 2) return launch_part_as<L, 2>(t, ctx, a, p);
-    return launch_part_as<L, PNV>(t, ctx, a, p);
+    // AUTO's miss-heavy intervals run the region variant (no count pass); IGX_GB_PART keeps
+    // exact runs, whose split work items also take heavily skewed streams in stride
+    const bool region = (t->mode == IGX_GB_AUTO || std::getenv("IGX_GBP_REGION")) && !std::getenv("IGX_GBP_EXACT");
+    if (nv == 0) return launch_part_as<L, 0>(t, ctx, a, p, region);
+    if (nv <= 2) return launch_part_as<L, 2>(t, ctx, a, p, region);
+    return launch_part_as<L, PNV>(t, ctx, a, p, region);
 }
 
 // one update over layout L in the interval's form

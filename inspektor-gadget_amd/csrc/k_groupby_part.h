@@ -82,6 +82,11 @@ struct PartArgs {
     uint32_t maxp;             // LDS probes before a row takes the HBM path
     uint32_t combine;          // wave pre-combine rounds per 64 records (0 = off)
     uint32_t dbg;              // diagnostics (IGX_GBP_DEBUG): phases to skip, results invalid
+    // region variant (no count pass): bucket b's records fill a fixed region of reg records
+    // through a cursor (one atomic per (tile, bucket)); a record past its region merges into
+    // the table directly (find-or-insert + atomics: exact on any stream)
+    uint32_t *rc1, *rc2;       // F1 / NB region cursors (records reserved; may pass the region)
+    uint32_t reg1, reg2;       // records per first-level / final region (0: exact runs)
 };
 
 // record words (compile-time bound): packed key words, loaded columns, index
@@ -354,6 +359,20 @@ __global__ __launch_bounds__(PTA) void k_gbp_offs(PartArgs p) {
     scan_column(p.cnt1 + (uint64_t)t0 * F1 + threadIdx.x, F1, t1 - t0, p.csum[(uint64_t)c * F1 + threadIdx.x]);
 }
 
+template <int KW, int NA>
+__device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
+                                          const uint64_t (&v)[NA], uint64_t first);
+
+// a staged record that found its region full: merged into the table directly (exact, slow;
+// never on a hashed stream whose buckets stay within 1.25x their share)
+template <int KW>
+__device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p, const uint32_t *rec) {
+    uint32_t k[KW];
+    uint64_t v[AMAX], gidx;
+    lds_decode<KW, AMAX>(a, p, rec, k, v, gidx);
+    hbm_merge<KW, AMAX>(a, k, hash_key<KW>(k), v, gidx);
+}
+
 // ---- A: a tile of rows -> records, each first-level bucket's run at its exact position -----
 // The tile's rows stay in registers (R per thread, all loads issued at once); a row's rank
 // in its bucket comes from an LDS atomic, so the records are staged in LDS already sorted
@@ -372,7 +391,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     const uint32_t t = blockIdx.x;
     if (threadIdx.x < F) {
         hist[threadIdx.x] = 0;
-        base[threadIdx.x] = p.cnt1[(uint64_t)t * F + threadIdx.x];
+        if (!p.reg1) base[threadIdx.x] = p.cnt1[(uint64_t)t * F + threadIdx.x];
     }
     __syncthreads();
     const uint64_t r0 = (uint64_t)t * TRA;
@@ -395,7 +414,11 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     __syncthreads();
     uint32_t total;
     const uint32_t o = block_excl_scan(threadIdx.x < F ? hist[threadIdx.x] : 0u, wsum, total);
-    if (threadIdx.x < F) off[threadIdx.x] = o;
+    if (threadIdx.x < F) {
+        off[threadIdx.x] = o;
+        const uint32_t hc = hist[threadIdx.x];   // region variant: this tile's run at the bucket's cursor
+        if (p.reg1) base[threadIdx.x] = hc ? atomicAdd(p.rc1 + threadIdx.x, hc) : 0u;
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -412,7 +435,60 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     for (uint32_t qi = threadIdx.x; qi < nq; qi += PTA) {
         const uint32_t j = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
         const uint32_t q = qi - j * rq, b = sb[j];
-        out[(uint64_t)(base[b] + j - off[b]) * rq + q] = stage[qi];
+        const uint32_t g = base[b] + j - off[b];
+        if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
+        else if (g < p.reg1) out[((uint64_t)b * p.reg1 + g) * rq + q] = stage[qi];
+        else if (q == 0) region_spill<KW>(a, p, reinterpret_cast<const uint32_t *>(stage + (uint64_t)j * rq));
+    }
+}
+
+// region variant, between A and B: B tiles of each first-level region (tstart, bt, ctl[1])
+__global__ __launch_bounds__(1024) void k_gbr_tiles(PartArgs p) {
+    __shared__ uint32_t wsum[17];
+    __shared__ uint32_t ts[PART_F_MAX + 1];
+    const uint32_t F1 = 1u << p.f1;
+    const uint32_t c = threadIdx.x < F1 ? min(p.rc1[threadIdx.x], p.reg1) : 0u;
+    uint32_t tot;
+    const uint32_t st = block_excl_scan((c + p.trb - 1) / p.trb, wsum, tot);
+    if (threadIdx.x < F1) {
+        p.tstart[threadIdx.x] = st;
+        ts[threadIdx.x] = st;
+    }
+    if (threadIdx.x == 0) {
+        p.tstart[F1] = tot;
+        ts[F1] = tot;
+        p.ctl[1] = tot;
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tot; t += 1024) p.bt[t] = upper_bound_u32(ts, 0, F1 + 1, t) - 1;
+}
+
+// region variant, after B: C work items from the final regions' fills (a final bucket larger
+// than ch is split)
+__global__ __launch_bounds__(1024) void k_gbr_items(PartArgs p) {
+    __shared__ uint32_t wsum[17];
+    const uint32_t NB = 1u << p.lb;
+    const uint32_t per = (NB + 1023) / 1024, b0 = threadIdx.x * per;
+    uint32_t si = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t b = b0 + i;
+        const uint32_t c = b < NB ? min(p.rc2[b], p.reg2) : 0u;
+        si += (c + p.ch - 1) / p.ch;
+    }
+    uint32_t toti;
+    uint32_t runi = block_excl_scan(si, wsum, toti);
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t b = b0 + i;
+        if (b >= NB) break;
+        const uint32_t c = min(p.rc2[b], p.reg2), ni = (c + p.ch - 1) / p.ch;
+        p.istart[b] = runi;
+        for (uint32_t k = 0; k < ni; ++k) p.itfb[runi + k] = b;
+        runi += ni;
+    }
+    if (threadIdx.x == 0) {
+        p.istart[NB] = toti;
+        p.ctl[0] = 0;
+        p.ctl[2] = toti;
     }
 }
 
@@ -434,8 +510,10 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
     const uint32_t b1 = p.bt[tile];
     const uint32_t j = tile - p.tstart[b1];
-    const uint32_t s = p.start2[b1 << p.f2] + j * trb;
-    const uint32_t e = min(p.start2[(b1 + 1) << p.f2], s + trb);
+    // exact runs: first-level bucket b1 spans final buckets' starts; regions: [b1 reg1, + fill)
+    const uint32_t s = p.reg1 ? b1 * p.reg1 + j * trb : p.start2[b1 << p.f2] + j * trb;
+    const uint32_t e = p.reg1 ? b1 * p.reg1 + min(min(p.rc1[b1], p.reg1), (j + 1) * trb)
+                              : min(p.start2[(b1 + 1) << p.f2], s + trb);
     const uint32_t cnt = e - s;
     if (threadIdx.x < F) hist[threadIdx.x] = 0;
     const u4v *src = reinterpret_cast<const u4v *>(p.recs1) + (uint64_t)s * rq;
@@ -463,7 +541,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     const uint32_t o = block_excl_scan(c, wsum, total);
     if (threadIdx.x < F) {
         off[threadIdx.x] = o;
-        base[threadIdx.x] = c ? atomicAdd(p.cur2 + (b1 << p.f2) + threadIdx.x, c) : 0u;
+        base[threadIdx.x] = c ? atomicAdd((p.reg2 ? p.rc2 : p.cur2) + (b1 << p.f2) + threadIdx.x, c) : 0u;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += PTA) perm[off[bkt[i]] + rank[i]] = (uint16_t)i;
@@ -474,7 +552,10 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
         const uint32_t jj = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
         const uint32_t q = qi - jj * rq;
         const uint32_t sidx = perm[jj], b = bkt[sidx];
-        out[(uint64_t)(base[b] + jj - off[b]) * rq + q] = stage[sidx * rq + q];
+        const uint32_t g = base[b] + jj - off[b];
+        if (!p.reg2) out[(uint64_t)g * rq + q] = stage[sidx * rq + q];
+        else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * rq + q] = stage[sidx * rq + q];
+        else if (q == 0) region_spill<KW>(a, p, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
     }
 }
 
@@ -735,7 +816,8 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         if (it >= nitems) break;
         const uint32_t fb = p.itfb[it];
         const uint32_t i0 = p.istart[fb], nit = p.istart[fb + 1] - i0, kx = it - i0;
-        const uint32_t s0 = p.start2[fb], len = p.start2[fb + 1] - s0;
+        const uint32_t s0 = p.reg2 ? fb * p.reg2 : p.start2[fb];
+        const uint32_t len = p.reg2 ? min(p.rc2[fb], p.reg2) : p.start2[fb + 1] - s0;
         const uint32_t s = s0 + (uint32_t)((uint64_t)len * kx / nit);
         const uint32_t e = s0 + (uint32_t)((uint64_t)len * (kx + 1) / nit);
         const uint64_t qlast = (uint64_t)e * rq - 1;   // the item's last quad (loads clamp to it)

@@ -474,7 +474,7 @@ def test_direct_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layou
     tab.destroy()
 
 
-@pytest.mark.parametrize("variant", ["plain", "skewed", "lds_overflow", "index_column"])
+@pytest.mark.parametrize("variant", ["plain", "skewed", "lds_overflow", "index_column", "region", "region_overflow"])
 @pytest.mark.parametrize("layout", ["tcp", "file", "np_distinct", "generic"])
 def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layout, variant):
     """IGX_GB_PART (k_groupby_part.h: count, scan, scatter into hash buckets, LDS aggregation
@@ -483,8 +483,15 @@ def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, 
     running base index and a nil mask.  'skewed': one key holds a large share of the rows, so
     its bucket is split into several work items that merge with CAS claims and atomics;
     'lds_overflow': an 8-entry LDS table sends most rows down the HBM path; 'index_column':
-    global indices from a u64 column (the owner-side merge of igx_dist_exchange_groups)."""
+    global indices from a u64 column (the owner-side merge of igx_dist_exchange_groups).
+    'region' / 'region_overflow': the region variant AUTO runs (no count pass, buckets filled
+    through cursors), the second with regions of 600 records so that most records take the
+    direct find-or-insert path from passes A and B."""
     A = igx._abi
+    if variant.startswith("region"):
+        monkeypatch.setenv("IGX_GBP_REGION", "1")
+    if variant == "region_overflow":
+        monkeypatch.setenv("IGX_GBP_REGSIZE", "600")
     n = 450_000
     rng = np.random.default_rng(11)
     s = 1.3 if variant == "skewed" else 0.5
