@@ -18,6 +18,7 @@
 // histogram -> scan -> stable scatter (wave64 ballot multi-split ranks, tile order kept
 // by per-digit running counters in LDS).  Words below the current digit are no longer
 // carried (LSD never reads them again).
+#include <cstdlib>
 #include <vector>
 
 #include "k_common.h"
@@ -34,6 +35,7 @@ struct ComposeArgs {
     const uint8_t *ptr[NSK];
     uint32_t width[NSK], kind[NSK], desc[NSK], words[NSK], rstride[NSK], direct[NSK];   // direct: read at i, not rowmap[i]
     uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
+    uint32_t reverse;     // pos_words == 0: slot i holds row n-1-i (the position order is descending)
     const uint64_t *pos;
     const uint8_t *valid;
     const uint32_t *rowmap;
@@ -54,9 +56,10 @@ __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, ui
 
 __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
                                                 uint32_t *__restrict__ payload) {
-    uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= a.n || (a.d_n && i >= *a.d_n)) return;
-    const uint64_t src = a.rowmap ? a.rowmap[i] : i;   // where row i's values live
+    const uint64_t r = a.reverse ? a.n - 1 - i : i;     // the row composed into slot i
+    const uint64_t src = a.rowmap ? a.rowmap[r] : r;   // where its values live
     bool nil = a.valid && a.valid[src] == 0;
     uint32_t w = 0;
     if (a.has_nil) words[(w++) * a.stride + i] = nil ? 1u : 0u;
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
             continue;
         }
         const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
-        const uint8_t *p = a.ptr[k] + (a.direct[k] ? i : src) * a.rstride[k];
+        const uint8_t *p = a.ptr[k] + (a.direct[k] ? r : src) * a.rstride[k];
         if (a.kind[k] == IGX_KIND_BYTES) {
             for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
@@ -106,7 +109,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
     if (a.pos_words == 2) {
         words[w * a.stride + i] = (uint32_t)(p >> 32);
         words[(w + 1) * a.stride + i] = (uint32_t)p;
-    } else {
+    } else if (a.pos_words == 1) {
         words[w * a.stride + i] = (uint32_t)p;
     }
     payload[i] = (uint32_t)src;
@@ -851,7 +854,14 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     ca.d_n = d_nrows;
     bool any_float = false;
     for (uint32_t k = 0; k < nkeys; ++k) any_float = any_float || keys[k].kind == IGX_KIND_FLOAT;
-    const uint32_t pos_words = (pos == nullptr) ? 1 : 2;
+    // A full sort by row order (no position column, no nil mask) needs no position words: the
+    // LSD passes are stable, so composing the rows in the tie order -- ascending, or reversed
+    // when the parity makes it descending -- orders the ties without passes of their own.  (A
+    // top-K keeps them: the selection needs unique keys.)
+    const bool sel_shape = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
+    const bool drop_pos = pos == nullptr && valid == nullptr && !sel_shape && !std::getenv("IGX_SORT_POSWORDS");
+    const uint32_t pos_words = drop_pos ? 0 : (pos == nullptr ? 1 : 2);
+    ca.reverse = drop_pos && pos_not ? 1u : 0u;
     KW += pos_words;
     if (KW > MAXW) return igx_fail(ctx, IGX_ENOTSUP, "sort: composed key too wide");
     ca.nkeys = nkeys;
@@ -892,6 +902,12 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     ca.nan_seen = res + 2 * KW;
     IGX_HIP(ctx, hipMemsetAsync(ca.nan_seen, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
+    if (KW == 0) {   // no key and no position words: the (possibly reversed) row order itself
+        const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+        IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[0], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        IGX_HIP(ctx, hipGetLastError());
+        return IGX_OK;
+    }
     const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
     uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
     hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);

@@ -19,7 +19,7 @@ timeout -k 10 200 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum --kernel-tra
 T=tools/pmc_traffic.py
 python3 $T --fetch $O/fetch --write $O/write --kernel 'StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>, false' --config '{"events": 100000000, "keys": 1000000, "zipf": 1.1}' --out $O/traffic_c2.json &&
 python3 $T --fetch $O/fetch --write $O/write --kernel 'k_hist<' --config '{"events": 125000000}' --out $O/traffic_c3.json &&
-python3 $T --fetch $O/fetch --write $O/write --kernel 'k_gbp_' --anchor 'k_gbp_count<' --extra k_np_mark --config '{"events": 125000000}' --out $O/traffic_c4.json &&
+python3 $T --fetch $O/fetch --write $O/write --kernel 'k_gb' --anchor 'k_gbp_a<' --extra k_np_mark --config '{"events": 125000000}' --out $O/traffic_c4.json &&
 python3 $T --fetch $O/fetch --write $O/write --kernel 'StaticLayout<8, 4, 4, 4>, false' --config '{"events": 125000000, "keys": 10000000}' --out $O/traffic_c5.json || { echo "traffic parse failed"; exit 1; }
 python3 tools/pmc_summary.py --kernel 'StaticLayout<16, 16, 8, 4, 16, 2, 2, 2>, false' $O/tcc1 $O/tcc2 $O/tcc3 $O/tcc4 > $O/tcc_c2.txt 2>&1 || echo "tcc summary failed"
 cp $O/trace/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null || find $O/trace -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
