@@ -101,6 +101,7 @@ extern "C" int igx_close(igx_ctx *ctx) {
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     for (auto &r : ctx->regex) (void)hipFree(r.second);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
+    if (ctx->nan_word) (void)hipFree(ctx->nan_word);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
     return IGX_OK;

@@ -27,6 +27,8 @@ struct igx_ctx {
     std::map<std::string, void *> regex;
     // igx_set_stream: the new stream waits on this event recorded on the old one
     hipEvent_t handoff = nullptr;
+    // the sort's NaN flag: one device word, zero between sorts (k_andor_final clears it)
+    uint32_t *nan_word = nullptr;
 };
 
 // sets ctx->err and returns code

@@ -43,6 +43,8 @@
 #include <utility>
 #include <vector>
 
+#include <thread>
+
 #include "k_common.h"
 
 // event-stream loads of the group-by kernels: non-temporal (read once; IGX_GB_STREAM_NT=0
@@ -834,7 +836,10 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
             }
             const uint64_t val = r.hi[p % ARING];
             const uint32_t slot = (uint32_t)w, what = (uint32_t)(w >> 32) & 15u;
-            if (!(DBG && (a.dbg & 4u))) {
+            if (DBG && (a.dbg & 131072u)) {   // diagnostics: plain stores instead of the atomics
+                if (what == WHAT_MIN) *rec_first(a, slot) = val;
+                else *rec_agg(a, slot, (int)what) = val;
+            } else if (!(DBG && (a.dbg & 4u))) {
                 if (what == WHAT_MIN) gmin(rec_first(a, slot), val);
                 else gadd(rec_agg(a, slot, (int)what), val);
             }
@@ -1348,7 +1353,23 @@ __global__ __launch_bounds__(256) void k_slots_count(const uint32_t *__restrict_
     if (threadIdx.x == 0) cnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
 }
 
-__global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, uint64_t m, uint64_t *__restrict__ total) {
+// finalize's read-back, written by the kernel that knows the group count straight into the
+// table's coherent pinned buffer (no copy after it): err block {bits, pad, LDS misses}, count
+// (then, released after them, the finalize's sequence number: the host polls it instead of
+// recording an event, whose release would flush L2 between finalize and the top-K)
+__device__ __forceinline__ void fin_export(const uint32_t *err, uint64_t total, uint64_t *host, uint64_t seq) {
+    const uint64_t e0 = *reinterpret_cast<const volatile uint64_t *>(err);
+    const uint64_t e1 = *reinterpret_cast<const volatile uint64_t *>(err + 2);
+    __hip_atomic_store(host, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(host + 3, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, uint64_t m, uint64_t *__restrict__ total,
+                                                     const uint32_t *__restrict__ err, uint64_t *__restrict__ host,
+                                                     uint64_t seq) {
     __shared__ uint32_t part[1024];
     const uint64_t per = (m + 1023) / 1024;
     const uint64_t b = threadIdx.x * per, e = min(m, b + per);
@@ -1368,12 +1389,23 @@ __global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, u
         v[i] = run;
         run += c;
     }
-    if (threadIdx.x == 1023) *total = part[1023];
+    if (threadIdx.x == 1023) {
+        *total = part[1023];
+        fin_export(err, part[1023], host, seq);
+    }
 }
 
+// The tile's slot list, staged in LDS and written out as one contiguous run.  With off null
+// the tile's base is the sum of the counts of the tiles before it (read here: no scan kernel,
+// for tables of at most SLOTS_INLINE_TILES tiles), and the last tile writes the total.
+constexpr uint32_t SLOTS_INLINE_TILES = 4096;
 __global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict__ occ, uint64_t nwords,
-                                                     const uint32_t *__restrict__ off, uint32_t *__restrict__ out) {
-    __shared__ uint32_t wsum[4];
+                                                     const uint32_t *__restrict__ off, const uint32_t *__restrict__ cnt,
+                                                     uint32_t *__restrict__ out, uint64_t *__restrict__ total,
+                                                     const uint32_t *__restrict__ err, uint64_t *__restrict__ host,
+                                                     uint64_t seq) {
+    __shared__ uint32_t wsum[4], pre[4];
+    __shared__ uint32_t buf[256 * 32];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     uint32_t m = i < nwords ? occ[i] : 0u;
@@ -1385,15 +1417,42 @@ __global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict_
         if ((int)lane >= d) inc += x;
     }
     if (lane == 63) wsum[wave] = inc;
+    uint32_t base = 0;
+    if (off) {
+        base = off[blockIdx.x];
+    } else {
+        for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) base += cnt[j];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) base += __shfl_xor(base, d);
+        if (lane == 0) pre[wave] = base;
+    }
     __syncthreads();
-    uint32_t base = off[blockIdx.x] + inc - c;
-    for (uint32_t w = 0; w < wave; ++w) base += wsum[w];
+    if (!off) base = pre[0] + pre[1] + pre[2] + pre[3];
+    uint32_t loc = inc - c;
+    for (uint32_t w = 0; w < wave; ++w) loc += wsum[w];
+    const uint32_t tile_n = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     const uint32_t s0 = (uint32_t)(i * 32);
     while (m) {
         const uint32_t bit = (uint32_t)__ffs(m) - 1;
-        out[base++] = s0 + bit;
+        buf[loc++] = s0 + bit;
         m &= m - 1;
     }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < tile_n; j += 256) out[base + j] = buf[j];
+    if (!off && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        *total = (uint64_t)base + tile_n;
+        fin_export(err, (uint64_t)base + tile_n, host, seq);
+    }
+}
+
+// an interval's reset: the occupancy bitmap and the error block in one launch
+__global__ __launch_bounds__(256) void k_reset_clear(uint32_t *__restrict__ occ, uint64_t nwords,
+                                                     uint32_t *__restrict__ err) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t n4 = nwords / 4;
+    for (uint64_t q = i; q < n4; q += (uint64_t)gridDim.x * 256) reinterpret_cast<uint4 *>(occ)[q] = make_uint4(0, 0, 0, 0);
+    if (i < (nwords & 3)) occ[n4 * 4 + i] = 0;
+    if (i < 4) err[i] = 0;
 }
 
 // materialise selected groups as packed rows key | aggs | first (the Stats rows of
@@ -1475,8 +1534,9 @@ struct igx_table {
     uint8_t *p_mask = nullptr;   // row mask of the predicates that are not fused (grow-only)
     size_t p_mask_bytes = 0;
     uint64_t host_groups = 0;
-    uint64_t *fin_host = nullptr;   // pinned: group count, error word, LDS misses (finalize read-back)
-    hipEvent_t fin_ev = nullptr;    // recorded after an asynchronous finalize's read-back copies
+    uint64_t *fin_host = nullptr;   // pinned, coherent: error word, LDS misses, group count (finalize read-back)
+    uint64_t *fin_dev = nullptr;    // the same buffer as the kernels address it
+    uint64_t fin_seq = 0;           // the last finalize's number (fin_host[3] once it has landed)
     bool fin_pending = false;       // igx_groupby_finalize_async not yet collected
     int fin_status = 0;             // status of a collected asynchronous finalize, not yet returned
     unsigned long long *dbg_cnt = nullptr;
@@ -1583,10 +1643,12 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
     t->occ_words = (ns + 31) / 32;
     if (e == hipSuccess) e = hipMalloc(&t->occ, t->occ_words * 4);
-    if (e == hipSuccess) e = hipMalloc(&t->n_groups, 64);
+    if (e == hipSuccess) t->n_groups = reinterpret_cast<uint64_t *>(t->err + 4);   // behind the error block
     if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&t->fin_host), 32, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->fin_ev, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&t->fin_host), 32, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&t->fin_dev), t->fin_host, 0);
+    if (e == hipSuccess) std::fill(t->fin_host, t->fin_host + 4, 0ull);
     if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream);
     if (e != hipSuccess) {
         igx_groupby_destroy(t);
@@ -1597,6 +1659,9 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
 }
 
 static int fin_collect(igx_table *t, uint64_t *n_groups);
+static bool fin_landed(const igx_table *t) {
+    return __atomic_load_n(t->fin_host + 3, __ATOMIC_ACQUIRE) == t->fin_seq;
+}
 
 extern "C" int igx_groupby_reset(igx_table *t) {
     if (!t) return IGX_EINVAL;
@@ -1605,7 +1670,7 @@ extern "C" int igx_groupby_reset(igx_table *t) {
     // bookkeeping then steers this interval); one still in flight is collected by a later
     // call, so a reset never waits for the device.  A collected error is returned after the
     // reset is done.
-    if (t->fin_pending && hipEventQuery(t->fin_ev) == hipSuccess) (void)fin_collect(t, nullptr);
+    if (t->fin_pending && fin_landed(t)) (void)fin_collect(t, nullptr);
     const int pending_rc = t->fin_status;
     t->fin_status = IGX_OK;
     // A new interval is a new epoch: records of older epochs read as empty and a claimer
@@ -1616,8 +1681,10 @@ extern "C" int igx_groupby_reset(igx_table *t) {
         IGX_HIP(ctx, hipGetLastError());
         t->ep = 1;
     }
-    IGX_HIP(ctx, hipMemsetAsync(t->occ, 0, t->occ_words * 4, ctx->stream));
-    IGX_HIP(ctx, hipMemsetAsync(t->err, 0, 16, ctx->stream));   // error bits + LDS-miss count
+    // the bitmap, the error bits and the LDS-miss count
+    hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)std::min<uint64_t>(1024, (t->occ_words / 4 + 255) / 256 + 1)), dim3(256),
+                       0, ctx->stream, t->occ, t->occ_words, t->err);
+    IGX_HIP(ctx, hipGetLastError());
     t->rows_fed = 0;
     t->host_groups = 0;
     return pending_rc;
@@ -1632,14 +1699,12 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->groups);
     (void)hipFree(t->tile_cnt);
     (void)hipFree(t->occ);
-    (void)hipFree(t->n_groups);
     (void)hipFree(t->dbg_cnt);
     (void)hipFree(t->p_recs);
     (void)hipFree(t->p_cnt);
     (void)hipFree(t->p_mask);
     for (auto *p : t->text) (void)hipFree(p);
     if (t->fin_host) (void)hipHostFree(t->fin_host);
-    if (t->fin_ev) (void)hipEventDestroy(t->fin_ev);
     delete t;
     return IGX_OK;
 }
@@ -1677,6 +1742,14 @@ static void launch_gb(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
             return;
         }
     }
+#ifdef IGX_GB_DEBUG_FILE
+    if constexpr (std::is_same<L, StaticLayout<8, 4, 4, 4>>::value) {
+        if (a.dbg) {
+            launch_gb_as<L, true, AMAX>(ctx, a, blocks);
+            return;
+        }
+    }
+#endif
     if (a.naggs <= 2) launch_gb_as<L, false, 2>(ctx, a, blocks);
     else launch_gb_as<L, false, AMAX>(ctx, a, blocks);
 }
@@ -2235,12 +2308,18 @@ static int fin_launch(igx_table *t) {
                            t->krec, t->krec_len, t->koff, t->nslots, t->ep, t->occ);
     hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                        t->tile_cnt);
-    hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups);
-    hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
-                       t->tile_cnt, t->groups);
+    // the kernel that finds the group count also writes the read-back into fin_host
+    const uint64_t seq = ++t->fin_seq;
+    if (tiles <= SLOTS_INLINE_TILES) {
+        hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
+                           (const uint32_t *)nullptr, t->tile_cnt, t->groups, t->n_groups, t->err, t->fin_dev, seq);
+    } else {
+        hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups, t->err,
+                           t->fin_dev, seq);
+        hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
+                           t->tile_cnt, (const uint32_t *)nullptr, t->groups, (uint64_t *)nullptr, t->err, t->fin_dev, seq);
+    }
     IGX_HIP(ctx, hipGetLastError());
-    IGX_HIP(ctx, hipMemcpyAsync(t->fin_host, t->n_groups, 8, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipMemcpyAsync(t->fin_host + 1, t->err, 16, hipMemcpyDeviceToHost, ctx->stream));
     return IGX_OK;
 }
 
@@ -2263,10 +2342,10 @@ static void fin_view(igx_table *t, igx_table_view *view, uint64_t ng) {
 // the interval's status
 static int fin_apply(igx_table *t) {
     igx_ctx *ctx = t->ctx;
-    const uint64_t *h = t->fin_host;
-    const uint64_t ng = h[0];
-    const uint32_t err = reinterpret_cast<const uint32_t *>(h)[2];
-    const uint64_t misses = h[2];
+    const uint64_t *h = t->fin_host;   // err block {bits, pad, LDS misses} | group count
+    const uint32_t err = reinterpret_cast<const uint32_t *>(h)[0];
+    const uint64_t misses = h[1];
+    const uint64_t ng = h[2];
     t->host_groups = ng;
     // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
     // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When
@@ -2289,7 +2368,16 @@ static int fin_apply(igx_table *t) {
 static int fin_collect(igx_table *t, uint64_t *n_groups) {
     if (t->fin_pending) {
         t->fin_pending = false;
-        IGX_HIP(t->ctx, hipEventSynchronize(t->fin_ev));
+        // poll the sequence number; once the stream has drained it must be there
+        while (!fin_landed(t)) {
+            const hipError_t q = hipStreamQuery(t->ctx->stream);
+            if (q == hipSuccess) {
+                if (fin_landed(t)) break;
+                return t->fin_status = igx_fail(t->ctx, IGX_EIO, "groupby: finalize read-back did not land");
+            }
+            if (q != hipErrorNotReady) IGX_HIP(t->ctx, q);
+            std::this_thread::yield();
+        }
         const int rc = fin_apply(t);
         if (rc && !t->fin_status) t->fin_status = rc;
     }
@@ -2317,7 +2405,6 @@ extern "C" int igx_groupby_finalize_async(igx_table *t, igx_table_view *view) {
     (void)fin_collect(t, nullptr);   // the previous one landed long ago (it precedes this interval)
     const int rc = fin_launch(t);
     if (rc) return rc;
-    IGX_HIP(ctx, hipEventRecord(t->fin_ev, ctx->stream));
     t->fin_pending = true;
     fin_view(t, view, 0);
     return IGX_OK;

@@ -41,7 +41,9 @@ struct ComposeArgs {
     const uint32_t *rowmap;
     const uint64_t *d_n;  // nullable: the row count on the device (n is then its upper bound)
     uint64_t n, stride;   // stride = words array pitch (elements)
-    uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN
+    uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN (k_andor_final
+                          // moves it into res and clears it: the word is the context's, zero
+                          // between sorts)
 };
 
 __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, uint32_t j) {
@@ -115,6 +117,32 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
     payload[i] = (uint32_t)src;
 }
 
+// The tables' SortStats shape: NK 8-byte integer keys (aggregates or the first index) read
+// through the slot list, the first index as the position, no nil mask.  Every load of a row
+// issues before any is used (the generic kernel's runtime key loop waits once per key).
+template <int NK>
+__global__ __launch_bounds__(TB) void k_compose_u64(ComposeArgs a, uint32_t *__restrict__ words,
+                                                    uint32_t *__restrict__ payload) {
+    const uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= a.n || (a.d_n && i >= *a.d_n)) return;
+    const uint64_t src = a.rowmap[i];
+    uint64_t v[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) v[k] = *reinterpret_cast<const uint64_t *>(a.ptr[k] + src * a.rstride[k]);
+    uint64_t ps = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(a.pos) + src * a.pos_stride);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const uint64_t inv = a.desc[k] ? ~0ull : 0ull;
+        const uint64_t x = (a.kind[k] == IGX_KIND_INT ? v[k] ^ (1ull << 63) : v[k]) ^ inv;
+        words[(uint64_t)(2 * k) * a.stride + i] = (uint32_t)(x >> 32);
+        words[(uint64_t)(2 * k + 1) * a.stride + i] = (uint32_t)x;
+    }
+    if (a.pos_not) ps = ~ps;
+    words[(uint64_t)(2 * NK) * a.stride + i] = (uint32_t)(ps >> 32);
+    words[(uint64_t)(2 * NK + 1) * a.stride + i] = (uint32_t)ps;
+    payload[i] = (uint32_t)src;
+}
+
 // per-word AND / OR over all rows -> part[(w * gridDim.x + block) * 2 + {0: and, 1: or}].
 // 16-byte loads, four in flight per lane; partials, not atomics: the words' results share
 // one line, and same-line atomics from every workgroup serialise at the memory side.
@@ -169,33 +197,43 @@ __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words
     }
 }
 
-// res[2*w], res[2*w+1] = AND / OR of word w's nb partials (one workgroup per word)
-__global__ __launch_bounds__(TB) void k_andor_final(const uint32_t *__restrict__ part, uint32_t nb,
-                                                    uint32_t *__restrict__ res) {
-    __shared__ uint32_t red[2][TB / 64];
-    const uint32_t w = blockIdx.x;
-    uint32_t va = 0xFFFFFFFFu, vo = 0;
-    for (uint32_t b = threadIdx.x; b < nb; b += TB) {
-        va &= part[2 * ((uint64_t)w * nb + b)];
-        vo |= part[2 * ((uint64_t)w * nb + b) + 1];
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        va &= __shfl_xor(va, o);
-        vo |= __shfl_xor(vo, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = va;
-        red[1][threadIdx.x >> 6] = vo;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int j = 1; j < TB / 64; ++j) {
-            va &= red[0][j];
-            vo |= red[1][j];
+struct SelState;
+__device__ void sel_state_init(const uint32_t *res, uint32_t nw, uint64_t n, uint32_t k, SelState *st,
+                               const uint64_t *d_n);
+
+// res[2w], res[2w + 1] = AND / OR of word w over k_andor's nb partials (one wave per word),
+// res[2 kw] = the NaN flag, which is cleared for the next sort.  With st (the device top-K)
+// the selection state is initialised from them too and its histogram cleared.
+__global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict__ part, uint32_t nb, uint32_t KW,
+                                                      uint32_t *__restrict__ res, uint32_t *__restrict__ nan_seen,
+                                                      SelState *st, uint64_t n, uint32_t k,
+                                                      const uint64_t *__restrict__ d_n, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t r[2 * MAXW];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t w = wave; w < KW; w += 1024 / 64) {
+        uint32_t va = 0xFFFFFFFFu, vo = 0;
+        for (uint32_t b = lane; b < nb; b += 64) {
+            va &= part[2 * ((uint64_t)w * nb + b)];
+            vo |= part[2 * ((uint64_t)w * nb + b) + 1];
         }
-        res[2 * w] = va;
-        res[2 * w + 1] = vo;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            va &= __shfl_xor(va, o);
+            vo |= __shfl_xor(vo, o);
+        }
+        if (lane == 0) {
+            res[2 * w] = r[2 * w] = va;
+            res[2 * w + 1] = r[2 * w + 1] = vo;
+        }
     }
+    if (threadIdx.x == 0) {
+        res[2 * KW] = *nan_seen;
+        *nan_seen = 0;
+    }
+    if (!st) return;
+    for (uint32_t b = threadIdx.x; b < (1u << 12); b += 1024) hist[b] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) sel_state_init(r, KW, n, k, st, d_n);
 }
 
 __global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ dw, uint32_t shift,
@@ -442,9 +480,8 @@ struct SelState {
     uint32_t bitpos, nbits, b, krem, n, acc_cnt, out_cnt, err;
 };
 
-__global__ void k_sel_init(const uint32_t *__restrict__ res, uint32_t nw, uint64_t n, uint32_t k, SelState *st,
-                           const uint64_t *__restrict__ d_n) {
-    if (threadIdx.x) return;
+__device__ void sel_state_init(const uint32_t *res, uint32_t nw, uint64_t n, uint32_t k, SelState *st,
+                               const uint64_t *d_n) {
     if (d_n) n = min(n, *d_n);
     uint32_t bitpos = nw * 32;
     for (uint32_t w = 0; w < nw; ++w) {
@@ -471,8 +508,21 @@ __global__ __launch_bounds__(TB) void k_sel_hist_d(const uint32_t *__restrict__ 
     if (n <= st->krem || nbits == 0) return;
     for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB) h[b] = 0;
     __syncthreads();
-    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < n; j += (uint64_t)gridDim.x * TB)
-        atomicAdd(&h[sel_digit(W, stride, nw, j, bitpos, nbits)], 1u);
+    // A table's sums are skewed: most groups share the lowest bins, and same-address LDS
+    // atomics serialise, so the lanes on the wave's first lane's bin add as one
+    for (uint64_t j0 = (uint64_t)blockIdx.x * TB; j0 < n; j0 += (uint64_t)gridDim.x * TB) {
+        const uint64_t j = j0 + threadIdx.x;
+        const bool live = j < n;
+        const uint32_t d = live ? sel_digit(W, stride, nw, j, bitpos, nbits) : 0xFFFFFFFFu;
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        const uint64_t same = __ballot(d == d0);
+        if (d == d0) {
+            if ((threadIdx.x & 63) == (uint32_t)__ffsll((long long)same) - 1 && d0 != 0xFFFFFFFFu)
+                atomicAdd(&h[d0], (uint32_t)__popcll(same));
+        } else if (live) {
+            atomicAdd(&h[d], 1u);
+        }
+    }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < SEL_BINS; b += TB)
         if (h[b]) atomicAdd(&hist[b], h[b]);
@@ -509,21 +559,49 @@ __device__ __forceinline__ void sel_pick_block(const uint32_t *hist, uint32_t kr
     __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_sel_pick(const uint32_t *__restrict__ hist, SelState *st) {
-    __shared__ uint32_t tmp[20];
-    if (st->n <= st->krem || st->nbits == 0) return;
-    uint32_t b, below, inb;
-    sel_pick_block(hist, st->krem, tmp, b, below, inb);
-    if (threadIdx.x == 0) st->b = b;
+// the bin holding the krem-th row, found by each split workgroup itself (TB threads x 16 bins;
+// the histogram is 16 KB in L2): no pick kernel between the histogram and the split
+__device__ __forceinline__ uint32_t sel_pick_tb(const uint32_t *__restrict__ hist, uint32_t krem, uint32_t *tmp) {
+    constexpr uint32_t PER = SEL_BINS / TB;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint4 *h4 = reinterpret_cast<const uint4 *>(hist + threadIdx.x * PER);
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER / 4; ++q) {
+        const uint4 x = h4[q];
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) s += v[j];
+    uint32_t inc = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += y;
+    }
+    if (lane == 63) tmp[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - s;
+    for (uint32_t q = 0; q < wave; ++q) run += tmp[q];
+    if (run < krem && run + s >= krem) {   // exactly one thread's bins cross krem
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            if (run < krem && run + v[j] >= krem) tmp[TB / 64] = threadIdx.x * PER + j;
+            run += v[j];
+        }
+    }
+    __syncthreads();
+    return tmp[TB / 64];
 }
 
 // grid-wide split of pass 1 (rows are 0..n-1): digit < b -> acc, digit == b -> out
 __global__ __launch_bounds__(TB) void k_sel_split_d(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
-                                                    SelState *st, uint32_t *__restrict__ acc,
-                                                    uint32_t *__restrict__ out) {
+                                                    SelState *st, const uint32_t *__restrict__ hist,
+                                                    uint32_t *__restrict__ acc, uint32_t *__restrict__ out) {
     const uint32_t n = st->n;
     if (n <= st->krem || st->nbits == 0) return;
-    const uint32_t bitpos = st->bitpos, nbits = st->nbits, b = st->b;
+    __shared__ uint32_t ptmp[TB / 64 + 1];
+    const uint32_t bitpos = st->bitpos, nbits = st->nbits, b = sel_pick_tb(hist, st->krem, ptmp);
     __shared__ uint32_t lcnt[2], gbase[2];
     if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
     __syncthreads();
@@ -566,7 +644,8 @@ __global__ __launch_bounds__(TB) void k_sel_split_d(const uint32_t *__restrict__
 // then acc holds exactly k rows
 __global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                      SelState *st, uint32_t *__restrict__ acc, uint32_t *cnd0,
-                                                     uint32_t *cnd1) {
+                                                     uint32_t *cnd1, uint32_t k, const uint32_t *__restrict__ payload,
+                                                     uint32_t *__restrict__ out) {
     __shared__ uint32_t h[SEL_BINS];
     __shared__ uint32_t tmp[20], cnt[2];
     uint32_t n = st->n, krem = st->krem, bitpos = st->bitpos, nbits = st->nbits, nacc = 0;
@@ -610,6 +689,33 @@ __global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict_
         __syncthreads();
     }
     for (uint32_t j = threadIdx.x; j < n; j += 1024) acc[nacc + j] = cand ? cand[j] : j;   // n == krem
+    if (!out) return;   // k x words > SEL_BINS: k_sel_rank ranks them
+    // rank of each accepted row among the others (full composed-key compare, as k_sel_rank)
+    // on an LDS copy of their words; output positions past the rows that exist read 0xFFFFFFFF
+    __syncthreads();
+    const uint32_t kk = min(k, st->n);
+    uint32_t *kw = h;   // the histogram is done with: kk x nw words
+    for (uint32_t q = threadIdx.x; q < kk * nw; q += 1024) {
+        const uint32_t r = q / nw, w = q % nw;
+        kw[q] = W[(uint64_t)w * stride + acc[r]];
+    }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < k; r += 1024) {
+        if (r >= kk) {
+            out[r] = 0xFFFFFFFFu;
+            continue;
+        }
+        uint32_t less = 0;
+        for (uint32_t j = 0; j < kk; ++j) {
+            int c = 0;
+            for (uint32_t w = 0; w < nw && c == 0; ++w) {
+                const uint32_t x = kw[j * nw + w], y = kw[r * nw + w];
+                c = x < y ? -1 : (x > y ? 1 : 0);
+            }
+            less += c < 0;
+        }
+        out[less] = payload[acc[r]];
+    }
 }
 
 // rank of acc[r] among the k accepted rows (full composed-key compare) -> out_perm
@@ -887,6 +993,10 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         return igx_fail(ctx, IGX_EINVAL, "sort: a device row count needs a top-K without float keys or nil mask");
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     static_assert(sizeof(SelState) <= 64 * 4, "SelState fits the 64 words before the selection histogram");
+    if (!ctx->nan_word) {
+        IGX_HIP(ctx, hipMalloc(&ctx->nan_word, 64));
+        IGX_HIP(ctx, hipMemsetAsync(ctx->nan_word, 0, 64, ctx->stream));
+    }
     void *s;
     int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b, &s);
     if (rc) return rc;
@@ -899,9 +1009,21 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     uint32_t *res = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b);
 
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
-    ca.nan_seen = res + 2 * KW;
-    IGX_HIP(ctx, hipMemsetAsync(ca.nan_seen, 0, 4, ctx->stream));
-    hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
+    ca.nan_seen = ctx->nan_word;
+    bool u64_shape = rowmap && pos && !valid && pos_words == 2 && nkeys >= 1 && nkeys <= 4;
+    for (uint32_t k = 0; k < nkeys && u64_shape; ++k)
+        u64_shape = (keys[k].kind == IGX_KIND_UINT || keys[k].kind == IGX_KIND_INT) && keys[k].width == 8 &&
+                    keys[k].words == 2 && !keys[k].direct;
+    if (u64_shape) {
+        switch (nkeys) {
+        case 1: hipLaunchKernelGGL(k_compose_u64<1>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+        case 2: hipLaunchKernelGGL(k_compose_u64<2>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+        case 3: hipLaunchKernelGGL(k_compose_u64<3>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+        default: hipLaunchKernelGGL(k_compose_u64<4>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+        }
+    } else {
+        hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
+    }
     if (KW == 0) {   // no key and no position words: the (possibly reversed) row order itself
         const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
         IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[0], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -911,28 +1033,36 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
     uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
     hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
-    hipLaunchKernelGGL(k_andor_final, dim3(KW), dim3(TB), 0, ctx->stream, apart, ablocks, res);
     if (use_sel && !any_float && rowmap) {
         // top-K of a table's groups without host round trips (SelState on the device): no float
         // key, so no NaN check; the first differing bit is found on the device; the position
-        // (first index) makes every composed key unique
+        // (first index) makes every composed key unique.  After the compose and AND/OR passes:
+        // the final AND/OR (which also initialises the selection), the first histogram, the
+        // split (each workgroup picks the bin itself) and the one-workgroup finish, which
+        // ranks the k rows itself when their words fit its LDS.
         uint32_t *acc = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b);
         uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
         SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
         uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
-        hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, ctx->stream, res, KW, nrows, limit, stp, d_nrows);
-        IGX_HIP(ctx, hipMemsetAsync(dh, 0, SEL_BINS * 4, ctx->stream));
-        const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, (nrows + TB - 1) / TB);
+        hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res, ctx->nan_word,
+                           stp, nrows, limit, d_nrows, dh);
+        // about 16 rows per thread: each workgroup adds its nonzero bins to the global
+        // histogram, and a skewed table's low bins take one same-address atomic per workgroup
+        const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, nrows / (16 * TB)));
         hipLaunchKernelGGL(k_sel_hist_d, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, stp, dh);
-        hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(1024), 0, ctx->stream, dh, stp);
         hipLaunchKernelGGL(k_sel_split_d, dim3((uint32_t)((nrows + TILE - 1) / TILE)), dim3(TB), 0, ctx->stream, W[0],
-                           stride, KW, stp, acc, cnd[0]);
-        hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0], cnd[1]);
-        hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
-                           out_perm, stp);
+                           stride, KW, stp, dh, acc, cnd[0]);
+        const bool fused = limit <= 1024 && (uint64_t)limit * KW <= SEL_BINS;   // the k rows' words fit its LDS
+        hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0], cnd[1],
+                           limit, P[0], fused ? out_perm : nullptr);
+        if (!fused)
+            hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
+                               out_perm, stp);
         IGX_HIP(ctx, hipGetLastError());
         return IGX_OK;
     }
+    hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res, ctx->nan_word,
+                       nullptr, nrows, limit, nullptr, nullptr);
     uint32_t *hres;
     rc = igx_pinned(ctx, KW * 8 + 4, reinterpret_cast<void **>(&hres));
     if (rc) return rc;

@@ -11,7 +11,7 @@ python3 - "$f" "$T" <<'PY'
 import csv, sys, re
 rows = list(csv.DictReader(open(sys.argv[1])))
 print("==", sys.argv[2])
-for r in rows[:14]:
+for r in rows[:int(__import__("os").environ.get("KT_ROWS","14"))]:
     n = re.sub(r"\(anonymous namespace\)::", "", r["Name"])
     n = re.sub(r"\((GbArgs|PartArgs|\(anonymous).*", "", n)[:70]
     print(f"{n:70s} {int(r['Calls']):4d} {float(r['AverageNs'])/1e3:9.1f} us")

@@ -32,6 +32,32 @@ __global__ void k_atomic(unsigned long long *tab, uint64_t words_per_region, uin
     }
 }
 
+// 32-bit adds (no return / returning) and 64-bit returning adds, same pattern
+template <int RET>
+__global__ void k_atomic32(unsigned int *tab, uint64_t words_per_region, uint64_t per, uint32_t *sink) {
+    const uint32_t x = xcc_id();
+    unsigned int *reg = tab + (uint64_t)x * words_per_region;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (uint64_t i = 0; i < per; ++i) {
+        const uint64_t r = mix(gid * per + i) % words_per_region;
+        if (RET) acc += __hip_atomic_fetch_add(&reg[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_add(&reg[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (acc == 0x12345678u) sink[0] = 1;
+}
+__global__ void k_atomic64r(unsigned long long *tab, uint64_t words_per_region, uint64_t per, uint32_t *sink) {
+    const uint32_t x = xcc_id();
+    unsigned long long *reg = tab + (uint64_t)x * words_per_region;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long acc = 0;
+    for (uint64_t i = 0; i < per; ++i) {
+        const uint64_t r = mix(gid * per + i) % words_per_region;
+        acc += __hip_atomic_fetch_add(&reg[r], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (acc == 0x12345678ull) sink[0] = 1;
+}
+
 // random plain 8-B loads within the XCD's region
 __global__ void k_load(const unsigned long long *tab, uint64_t words_per_region, uint64_t per, uint32_t *sink) {
     const uint32_t x = xcc_id();
@@ -104,7 +130,12 @@ int main() {
         hipMemcpy(&got, sum, 8, hipMemcpyDeviceToHost);
         float ml = timeit([&] { k_load<<<blocks, threads>>>(tab, w, per, sink); });
         float mr = timeit([&] { k_rmw<<<blocks, threads>>>(tab, w, per); });
+        float m32 = timeit([&] { k_atomic32<0><<<blocks, threads>>>((unsigned int *)tab, 2 * w, per, sink); });
+        float m32r = timeit([&] { k_atomic32<1><<<blocks, threads>>>((unsigned int *)tab, 2 * w, per, sink); });
+        float m64r = timeit([&] { k_atomic64r<<<blocks, threads>>>(tab, w, per, sink); });
         const double ops = (double)lanes * per;
+        printf("region %7.2f MiB x8: atomics u32 %6.1f G/s  u32 returning %6.1f G/s  u64 returning %6.1f G/s\n", rb / 1048576.0,
+               ops / m32 / 1e6, ops / m32r / 1e6, ops / m64r / 1e6);
         printf("region %7.2f MiB x8: atomics agent %6.1f G/s  workgroup %6.1f G/s (sum %s: %llu of %.0f)  loads %6.1f G/s  plain rmw %6.1f G/s\n",
                rb / 1048576.0, ops / ma / 1e6, ops / mw / 1e6, got == (unsigned long long)(2 * ops) ? "ok" : "MISMATCH", got,
                2 * ops, ops / ml / 1e6, ops / mr / 1e6);
