@@ -238,7 +238,7 @@ __global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict
 
 __global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ dw, uint32_t shift,
                                                    uint64_t n, uint32_t nblocks,
-                                                   uint32_t *__restrict__ hist) {
+                                                   uint32_t *__restrict__ hist, uint32_t tile_major) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -249,7 +249,8 @@ __global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ 
         if (i < n) atomicAdd(&h[(dw[i] >> shift) & 255u], 1u);
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (tile_major) hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+    else hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
 // Three-phase exclusive scan over m u32 values (the [digit][tile] histogram): per-chunk
@@ -344,8 +345,49 @@ struct ScatterArgs {
     uint64_t n;
     const uint32_t *pin;
     uint32_t *pout;
-    const uint32_t *off;  // scanned hist [256][nblocks]
+    const uint32_t *off;  // scanned hist [256][nblocks], or null: the prefetching kernel
+                          // scans the raw counts cnt ([nblocks][256]) itself (nblocks <= SCAN_FREE_TILES)
+    const uint32_t *cnt;
 };
+
+constexpr uint32_t SCAN_FREE_TILES = 512;
+
+// this tile's base of every digit from the raw counts, stored tile-major ([tile][digit]: a
+// wave reads 64 digits of one tile in one request): thread t sums digit t's counts over the
+// tiles before this one and over all tiles, then the digit totals are scanned across the
+// workgroup -- the three scan kernels a pass would otherwise need
+__device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t *tmp) {
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t pre = 0, tot = 0;
+    const uint32_t me = blockIdx.x;
+    uint32_t q = 0;
+    for (; q + 8 <= nb; q += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = cnt[(uint64_t)(q + u) * 256 + t];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            tot += v[u];
+            if (q + u < me) pre += v[u];
+        }
+    }
+    for (; q < nb; ++q) {
+        const uint32_t v = cnt[(uint64_t)q * 256 + t];
+        tot += v;
+        if (q < me) pre += v;
+    }
+    uint32_t inc = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += y;
+    }
+    if (lane == 63) tmp[wave] = inc;
+    __syncthreads();
+    uint32_t ex = inc - tot;
+    for (uint32_t w = 0; w < wave; ++w) ex += tmp[w];
+    return ex + pre;
+}
 
 __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
     __shared__ uint32_t base[256], running[256];
@@ -390,6 +432,72 @@ __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
     }
 }
 
+// The same pass for at most NLMAX live words: a row's words and payload are loaded one tile
+// row ahead, so their round trip overlaps the ballots and barriers of the row before (the
+// generic kernel loads them only at the write, after both barriers).
+template <int NLMAX>
+__global__ __launch_bounds__(TB) void k_radix_scatter_pf(ScatterArgs a) {
+    __shared__ uint32_t base[256], running[256], stmp[TB / 64];
+    __shared__ uint32_t wcnt[TB / 64][256], wpre[TB / 64][256];
+    const uint32_t t = threadIdx.x, wave = t >> 6;
+    base[t] = a.off ? a.off[(uint64_t)t * a.nblocks + blockIdx.x] : tile_digit_base(a.cnt, a.nblocks, stmp);
+    running[t] = 0;
+    for (int w = 0; w < TB / 64; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+    uint32_t cw[NLMAX], nw[NLMAX], cp = 0, np = 0;
+    auto load = [&](int j, uint32_t (&wv)[NLMAX], uint32_t &pv) {
+        const uint64_t i = tbase + (uint64_t)j * TB + t;
+        if (i < a.n) {
+#pragma unroll
+            for (int w = 0; w < NLMAX; ++w)
+                if ((uint32_t)w < a.nlive) wv[w] = a.in[w][i];
+            pv = a.pin[i];
+        }
+    };
+    load(0, cw, cp);
+    for (int j = 0; j < IPT; ++j) {
+        if (j + 1 < IPT) load(j + 1, nw, np);
+        const uint64_t i = tbase + (uint64_t)j * TB + t;
+        const bool valid = i < a.n;
+        uint32_t dv = 0;
+#pragma unroll
+        for (int w = 0; w < NLMAX; ++w)
+            if ((uint32_t)w == a.dword) dv = cw[w];
+        const uint32_t d = valid ? (dv >> a.shift) & 255u : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t rank = __popcll(peers & lanemask_lt());
+        if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
+        __syncthreads();
+        {
+            uint32_t r = running[t];
+#pragma unroll
+            for (int w = 0; w < TB / 64; ++w) {
+                wpre[w][t] = r;
+                r += wcnt[w][t];
+                wcnt[w][t] = 0;
+            }
+            running[t] = r;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint64_t pos = (uint64_t)base[d] + wpre[wave][d] + rank;
+#pragma unroll
+            for (int w = 0; w < NLMAX; ++w)
+                if ((uint32_t)w < a.nlive) a.out[w][pos] = cw[w];
+            a.pout[pos] = cp;
+        }
+#pragma unroll
+        for (int w = 0; w < NLMAX; ++w) cw[w] = nw[w];
+        cp = np;
+    }
+}
 
 // ---- top-K by radix select (k <= SEL_SMALL_K) -----------------------------------------
 // The composed keys are unique (the position word is part of them), so the k smallest
@@ -1162,10 +1270,18 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             sa.shift = 8 * b;
             sa.pin = P[cur];
             sa.pout = P[cur ^ 1];
+            const bool scan_free = nl <= 8 && nblocks <= SCAN_FREE_TILES;
             hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(TB), 0, ctx->stream,
-                               sa.in[dslot], sa.shift, nrows, nblocks, hist);
-            launch_scan(ctx->stream, hist, (uint64_t)256 * nblocks, scan_part);
-            hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+                               sa.in[dslot], sa.shift, nrows, nblocks, hist, scan_free ? 1u : 0u);
+            sa.off = scan_free ? nullptr : hist;
+            sa.cnt = hist;
+            if (!scan_free) launch_scan(ctx->stream, hist, (uint64_t)256 * nblocks, scan_part);
+            if (nl <= 4)
+                hipLaunchKernelGGL(k_radix_scatter_pf<4>, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+            else if (nl <= 8)
+                hipLaunchKernelGGL(k_radix_scatter_pf<8>, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+            else
+                hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
             // swap buffers: the next pass reads what this one wrote
             cur ^= 1;
             for (uint32_t l = 0; l < nl; ++l) {
