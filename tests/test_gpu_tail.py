@@ -1,0 +1,105 @@
+"""GPU parity of the step tail: the table top-K's device selection (every k regime: the
+finish ranks k <= 1024 rows itself, k_sel_rank above; the group count read on the device
+after igx_groupby_finalize_async), the slot list of tables past SLOTS_INLINE_TILES tiles
+(scan kernel) and below it (in-kernel prefix), and the radix passes on both sides of
+SCAN_FREE_TILES.  References: the oracle's Go SliceStable restatement over the canonical
+(first-occurrence) order -- SortStats, pkg/columns/sort/sort.go:35-83 -- and numpy.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def E(igx):
+    return igx.engine
+
+
+@pytest.fixture(scope="module")
+def H(igx):
+    return igx.columns
+
+
+def _go_top(oracle, first, cols, k):
+    """first indices of the top k groups: Go SliceStable over the first-occurrence order"""
+    order = np.argsort(first, kind="stable")
+    perm = oracle.go_sort_entries([(c[order], "uint64", d) for c, d in cols], len(first))
+    return first[order][perm.astype(np.int64)][:k]
+
+
+@pytest.mark.parametrize("sync", [True, False])
+def test_table_topk_every_k(oracle, E, H, igx, sync):
+    A = igx._abi
+    G, n = 8000, 400_000
+    ev_h = oracle.gen_tcp(0xC2, 0, G, oracle.zipf_cdf(G, 1.1), 0, n)
+    ev = {k: H.to_device(v) for k, v in ev_h.items()}
+    cols = [ev[k] for k in ("pid", "lport", "family")] + [ev["size"]]
+    aggs = [A.Agg(A.AGG_SUM, 3, A.NO_COL, 8, 0), A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)]
+    tab = E.Table([4, 2, 2], aggs, 2 * G)
+    tab.update(cols, [0, 1, 2], n, 0)
+    fin = tab.finalize()
+    _, ta, tf = E.table_tensors(tab, fin)
+    s, c, f = H.host(ta[0]), H.host(ta[1]), H.host(tf)
+    g = fin["n_groups"]
+    key_sets = {
+        "sum desc, count asc": ([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, False)], [(s, True), (c, False)]),
+        "count desc": ([(A.TSRC_AGG, 1, True)], [(c, True)]),
+        "first desc": ([(A.TSRC_FIRST, 0, True)], [(f, True)]),
+        "sum asc": ([(A.TSRC_AGG, 0, False)], [(s, False)]),
+    }
+    row_first = fin["key_bytes"] + 8 * 2   # packed row: key | 2 aggs | first
+    for name, (tkeys, okeys) in key_sets.items():
+        for k in (1, 20, 300, 1500, 4000):
+            if not sync:
+                tab.reset()
+                tab.update(cols, [0, 1, 2], n, 0)
+                assert tab.finalize(sync=False)["n_groups"] is None
+            rows = H.host(tab.gather(tab.sort(tkeys, k)))
+            if not sync:
+                assert tab.wait() == g
+            got = rows[:, row_first:row_first + 8].copy().view(np.uint64).ravel()
+            want = _go_top(oracle, f, okeys, k)
+            assert np.array_equal(got[:len(want)], want), (name, k)
+            assert not rows[len(want):].any(), (name, k)
+    tab.destroy()
+
+
+def test_large_table_slot_list(oracle, E, H, igx):
+    """a table of more than SLOTS_INLINE_TILES x 8192 slots: the slot list through the scan
+    kernel, the read-back from it, top-20 by count -- synchronous and asynchronous"""
+    A = igx._abi
+    rng = np.random.default_rng(11)
+    n, cap = 1_000_000, 30_000_000
+    keys = rng.integers(0, 600_000, n, dtype=np.uint32) * np.uint32(2654435761)
+    tab = E.Table([4], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], cap)
+    kd = H.to_device(keys)
+    tab.update([kd], [0], n, 0)
+    fin = tab.finalize()
+    assert fin["n_slots"] > 4096 * 8192
+    uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
+    assert fin["n_groups"] == len(uk)
+    tk, _, tf = E.table_tensors(tab, fin)
+    assert np.array_equal(np.sort(H.host(tk)[:, :4].copy().view(np.uint32).ravel()), uk)
+    want = _go_top(oracle, first.astype(np.uint64), [(cnt.astype(np.uint64), True)], 20)
+    for sync in (True, False):
+        tab.reset()
+        tab.update([kd], [0], n, 0)
+        tab.finalize(sync=sync)
+        rows = H.host(tab.gather(tab.sort([(A.TSRC_AGG, 0, True)], 20)))
+        if not sync:
+            assert tab.wait() == len(uk)
+        o = fin["key_bytes"] + 8   # packed row: key | count | first
+        assert np.array_equal(rows[:, o:o + 8].copy().view(np.uint64).ravel(), want)
+    tab.destroy()
+
+
+@pytest.mark.parametrize("n", [2_000_000, 2_200_000])   # 489 / 538 tiles: scan-free / scan kernels
+def test_radix_passes_both_scan_paths(oracle, E, H, n):
+    """SortEntries(["b", "-a"]) with ties: b asc, a desc, ties in reverse input order"""
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 1 << 20, n, dtype=np.uint32)
+    b = rng.integers(0, 64, n, dtype=np.uint32)
+    got = H.host(E.sort_perm([(H.to_device(b), False), (H.to_device(a), True)], n)).astype(np.int64)
+    want = oracle.go_sort_entries([(b, "uint32", False), (a, "uint32", True)], n).astype(np.int64)
+    assert np.array_equal(got, want)
