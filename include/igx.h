@@ -298,7 +298,10 @@ int igx_groupby_finalize(igx_table *t, igx_table_view *view);
  * tracer.go:177-226, with no wait in it).  The count and the status igx_groupby_finalize
  * would have returned (IGX_ENOSPC) come back from igx_groupby_wait, or from the first
  * igx_groupby_reset / igx_groupby_finalize that finds the read-back landed (a reset never
- * waits for the device).  Asynchronous. */
+ * waits for the device).  The read-back is written by the kernel that counts the groups into
+ * the table's coherent pinned buffer, followed by a sequence number the host polls (no copy
+ * and no event on the stream); igx_groupby_wait polls it, and fails with IGX_EIO if the
+ * stream drains without it.  Asynchronous. */
 int igx_groupby_finalize_async(igx_table *t, igx_table_view *view);
 /* Waits for the last igx_groupby_finalize_async: *n_groups (nullable) = its group count;
  * returns its status.  IGX_OK (and the last known count) when none is pending. */

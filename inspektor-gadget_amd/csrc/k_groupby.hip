@@ -724,7 +724,8 @@ __device__ __forceinline__ void lds_accumulate(const GbArgs &a, const LdsCache<K
     for (int x = 0; x < NA; ++x)
         if (x < (int)a.naggs && v[x])
             atomicAdd(reinterpret_cast<unsigned long long *>(&c.agg[x * c.E + slot]), (unsigned long long)v[x]);
-    atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
+    // rows arrive nearly in index order: a plain read skips most of the minima
+    if (gidx < c.first[slot]) atomicMin(reinterpret_cast<unsigned long long *>(&c.first[slot]), (unsigned long long)gidx);
 }
 
 // ---- HBM atomics through an LDS ring ---------------------------------------------------

@@ -763,13 +763,29 @@ __device__ __forceinline__ void wave_combine(const GbArgs &a, uint32_t rounds, b
 // 16-B quads (the next round's quads in registers while this round is aggregated from LDS).
 constexpr uint32_t UCMAX = 2;
 
+// The LDS table's set and tag need no relation to the table's hash (the records of an item
+// already share its top bits): a 32-bit multiply-xorshift of the key words, about a third of
+// hash_key's quarter-rate multiplies.  hash_key runs only where a group meets HBM.
+template <int KW>
+__device__ __forceinline__ uint64_t lds_hash(const uint32_t (&k)[KW]) {
+    uint32_t x = 0x9E3779B9u * (uint32_t)KW;
+#pragma unroll
+    for (int w = 0; w < KW; ++w) {
+        x = (x ^ k[w]) * 0x85EBCA6Bu;
+        x ^= x >> 13;
+    }
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+
 template <int KW, int NA>
 __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<KW> &T, bool ok,
                                       const uint32_t *rec) {
     uint32_t k[KW];
     uint64_t v[nax(NA)], gidx = 0;
     lds_decode<KW, NA>(a, p, rec, k, v, gidx);
-    const uint64_t hh = hash_key<KW>(k);
+    const uint64_t hh = lds_hash<KW>(k);
     if (p.combine) wave_combine<KW, nax(NA)>(a, p.combine, ok, k, hh, v, gidx);   // IGX_GBP_COMBINE
     if (!ok || (p.dbg & 32u)) return;
     const int ei = at_find_insert<KW>(T, k, hh, p.maxp);
@@ -779,10 +795,12 @@ __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const 
         for (int x = 0; x < NA; ++x)
             if (x < (int)a.naggs && v[x])
                 atomicAdd(reinterpret_cast<unsigned long long *>(&T.agg[(uint64_t)x * T.E + ei]), (unsigned long long)v[x]);
-        atomicMin(reinterpret_cast<unsigned long long *>(&T.first[ei]), (unsigned long long)gidx);
+        // records arrive nearly in index order: a plain read skips most of the minima (a
+        // read of one address from many lanes is a broadcast, an atomic a queue)
+        if (gidx < T.first[ei]) atomicMin(reinterpret_cast<unsigned long long *>(&T.first[ei]), (unsigned long long)gidx);
     } else {
         T.flag[0] = 1;
-        hbm_merge<KW, nax(NA)>(a, k, hh, v, gidx);
+        hbm_merge<KW, nax(NA)>(a, k, hash_key<KW>(k), v, gidx);
     }
 }
 

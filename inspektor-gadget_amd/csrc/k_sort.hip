@@ -47,6 +47,8 @@ struct ComposeArgs {
 };
 
 __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, uint32_t j) {
+    if (4 * j + 4 <= width && (reinterpret_cast<uintptr_t>(p) & 3) == 0)   // a whole aligned dword
+        return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(p + 4 * j));
     uint32_t v = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
