@@ -1525,6 +1525,8 @@ struct igx_table {
     bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
     uint32_t mode = IGX_GB_AUTO; // igx_groupby_set_mode
     uint32_t direct_left = 0;    // AUTO: intervals to run in the direct form before re-measuring
+    uint32_t region_off = 0;     // AUTO: intervals to partition exactly after a region overflowed
+    bool interval_region = false;   // the interval ran the region variant
     bool interval_direct = false;// the current interval's updates run the direct form
     bool interval_part = false;  // ... the partitioned form
     // partitioned form scratch (grow-only)
@@ -1654,6 +1656,11 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e != hipSuccess) {
         igx_groupby_destroy(t);
         return igx_fail(ctx, IGX_ENOMEM, "groupby_create: %s", hipGetErrorString(e));
+    }
+    // tuning / A-B knob (tools/gpu/ab_modes.sh): the initial mode, as igx_groupby_set_mode
+    if (const char *m = std::getenv("IGX_GB_MODE")) {
+        const unsigned long v = std::strtoul(m, nullptr, 0);
+        if (v <= IGX_GB_PART) t->mode = (uint32_t)v;
     }
     *out = t;
     return igx_groupby_reset(t);
@@ -2008,7 +2015,13 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
     }
     // AUTO's miss-heavy intervals run the region variant (no count pass); IGX_GB_PART keeps
     // exact runs, whose split work items also take heavily skewed streams in stride
-    const bool region = (t->mode == IGX_GB_AUTO || std::getenv("IGX_GBP_REGION")) && !std::getenv("IGX_GBP_EXACT");
+    // The region variant sizes each bucket's region at 1.25x its share of the rows; a bucket
+    // past it merges its extra records into the table one by one (exact, but a hot key's
+    // records then queue on one record's atomics).  An interval that overflowed a region
+    // switches AUTO to the exact variant for the rest of the partitioned run.
+    const bool region = (t->mode == IGX_GB_AUTO || std::getenv("IGX_GBP_REGION")) && !std::getenv("IGX_GBP_EXACT") &&
+                        t->region_off == 0;
+    t->interval_region = t->interval_region || region;
     if (nv == 0) return launch_part_as<L, 0>(t, ctx, a, p, region);
     if (nv <= 2) return launch_part_as<L, 2>(t, ctx, a, p, region);
     return launch_part_as<L, PNV>(t, ctx, a, p, region);
@@ -2261,6 +2274,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         t->interval_direct = t->mode == IGX_GB_DIRECT;
         t->interval_part = t->mode == IGX_GB_PART || (t->mode == IGX_GB_AUTO && t->direct_left > 0);
         if (t->mode == IGX_GB_AUTO && t->direct_left > 0) --t->direct_left;
+        t->interval_region = false;
+        if (t->region_off > 0) --t->region_off;
     }
     if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = t->interval_part = false;   // diagnostics: cached form
     int rc = IGX_OK;
@@ -2347,6 +2362,8 @@ static int fin_apply(igx_table *t) {
     const uint32_t err = reinterpret_cast<const uint32_t *>(h)[0];
     const uint64_t misses = h[1];
     const uint64_t ng = h[2];
+    const uint32_t spilled = reinterpret_cast<const uint32_t *>(h)[1];   // a region overflowed
+    if (spilled && t->interval_region) t->region_off = DIRECT_RUN + 1;
     t->host_groups = ng;
     // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
     // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When

@@ -367,6 +367,8 @@ __device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[K
 // never on a hashed stream whose buckets stay within 1.25x their share)
 template <int KW>
 __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p, const uint32_t *rec) {
+    // err block word 1: a region overflowed this interval (AUTO then partitions exactly)
+    if (!*reinterpret_cast<volatile const uint32_t *>(a.err + 1)) *reinterpret_cast<volatile uint32_t *>(a.err + 1) = 1u;
     uint32_t k[KW];
     uint64_t v[AMAX], gidx;
     lds_decode<KW, AMAX>(a, p, rec, k, v, gidx);
