@@ -103,3 +103,27 @@ def test_radix_passes_both_scan_paths(oracle, E, H, n):
     got = H.host(E.sort_perm([(H.to_device(b), False), (H.to_device(a), True)], n)).astype(np.int64)
     want = oracle.go_sort_entries([(b, "uint32", False), (a, "uint32", True)], n).astype(np.int64)
     assert np.array_equal(got, want)
+
+
+def test_auto_region_overflow_then_exact(E, H, igx):
+    """AUTO on a miss-heavy stream with one hot key: cached (measures), then the region
+    variant (the hot key's bucket overflows: its extra records merge one by one), then the
+    exact variant -- every interval's groups and the hot key's count exact"""
+    A = igx._abi
+    rng = np.random.default_rng(5)
+    n = 4_000_000
+    keys = rng.integers(1, 20_000_000, n, dtype=np.uint32)
+    keys[rng.random(n) < 0.05] = 0
+    uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
+    kd = H.to_device(keys)
+    tab = E.Table([4], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], 8_000_000)
+    for it in range(4):
+        tab.reset()
+        tab.update([kd], [0], n, 0)
+        fin = tab.finalize()
+        assert fin["n_groups"] == len(uk), it
+        row = H.host(tab.gather(tab.sort([(A.TSRC_AGG, 0, True)], 1)))[0]
+        o = fin["key_bytes"]
+        assert row[:4].view(np.uint32)[0] == 0 and row[o:o + 8].view(np.uint64)[0] == cnt[0], it
+        assert row[o + 8:o + 16].view(np.uint64)[0] == first[0], it
+    tab.destroy()
