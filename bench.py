@@ -4,8 +4,9 @@ SURVEY.md §8(d) configs in the same run.
 One headline step = one `top tcp` interval over a resident batch of synthetic events:
   reset the device table (the per-interval map drain, tracer.go:154-171)
   -> keyed group-by of every event on the 8-field ip_key_t, summing sent / recv, with the
-     probe's family set test fused in (tcptop.bpf.c:33-110; `family in {AF_INET, AF_INET6}`
-     :54-55 as an IGX_CMP_IN predicate, the same one gadgets.TopTcpTracer uses)
+     probes' checks fused in (tcptop.bpf.c:33-131; `family in {AF_INET, AF_INET6}` :54-55 as
+     an IGX_CMP_IN predicate, the receive probe's `copied <= 0` drop :127-128 as a guarded
+     `copied > 0`, the same ones gadgets.TopTcpTracer uses)
   -> stable top-20 by ["-sent","-recv"] with the reference's tie order (top.go:39-41)
   -> N>1: all-gather of the per-rank top-20 candidates over RCCL + exact global merge.
 Events are hash-partitioned across GPUs at ingest (each rank owns its own key universe),
@@ -82,7 +83,50 @@ def parse():
                    help="events per GPU for C3/C4/C5 (the 8-GPU configs' 1B / 8)")
     p.add_argument("--config-steps", type=int, default=5)
     p.add_argument("--check", action="store_true", help="verify the top-K against the oracle")
+    p.add_argument("--transport", choices=("igx", "torch"), default="igx",
+                   help="N>1 exchanges: the igx_dist_* C ABI over RCCL (falls back to torch's "
+                        "collectives if igx_dist_init fails on any rank) or torch's collectives")
+    p.add_argument("--launch-dry-run", action="store_true",
+                   help="launcher self-test: each rank prints its RANK/WORLD_SIZE and exits, no GPU")
     return p.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """`--gpus N` (N > 1) without a torch.distributed launcher: start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), before this process
+    makes any torch or HIP call.  Rank 0 prints the JSON line; the exit status is the first
+    failing rank's (the others are then terminated), else 0."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return status
 
 
 class Timer:
@@ -193,6 +237,15 @@ def family_in_pred(A, col):
     return p
 
 
+def copied_pred(A, col, dir_col):
+    """tcptop.bpf.c:124-130: the receive probe returns when `int copied <= 0`; sends have no
+    such check -- `copied > 0` guarded by dir == 1 (gadgets.copied_pred)."""
+    p = A.Pred()
+    p.col, p.cmp, p.negate, p.ref_len = col, A.CMP_GT, 0, 4
+    p.guard_col, p.guard_len, p.guard_ref[0] = dir_col, 1, 1
+    return p
+
+
 def run_c2(a, ctx):
     torch, E, H, A, D, T = ctx["torch"], ctx["E"], ctx["H"], ctx["A"], ctx["D"], ctx["timer"]
     rank, world = ctx["rank"], ctx["world"]
@@ -200,10 +253,10 @@ def run_c2(a, ctx):
     cdf_h = E.zipf_cdf(G, a.zipf)
     base = rank * N                                   # global event index of row 0
     ev = E.gen_tcp(0xC2, rank, G, H.to_device(cdf_h, ctx["dev"]), base, N)
-    cols = [ev[k] for k in TCP_NAMES]
+    cols = [ev[k] for k in TCP_NAMES] + [ev["size"].view(torch.int32)]   # 10: `int copied`
     aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
     tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2], aggs, capacity=G + G // 4)
-    preds = [family_in_pred(A, 7)]
+    preds = [family_in_pred(A, 7), copied_pred(A, 10, 9)]
     clk = KernelClock(torch)
     st = {}
 
@@ -509,14 +562,25 @@ def run_c5(a, ctx):
 
 def main():
     a = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            sys.exit(launch_ranks(a))
+    elif int(os.environ["WORLD_SIZE"]) != a.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.launch_dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world,
+                          "master": [os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]}), flush=True)
+        return
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    transport = None
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -524,6 +588,8 @@ def main():
     O = None
     if rank == 0 and world == 1 and (a.cpu_sample or a.check):
         from oracle import oracle as O   # CPU baselines / --check only (test infrastructure)
+    if world > 1:
+        transport = igx.dist.select_transport(a.transport)
     ctx = {"torch": torch, "igx": igx, "E": igx.engine, "H": igx.columns, "A": igx._abi, "D": igx.dist,
            "O": O, "rank": rank, "world": world, "dev": dev, "timer": Timer(torch, dist, world, dev)}
 
@@ -553,7 +619,9 @@ def main():
                             "pid,comm,lport,dport,family) sum sent/recv, stable top-20 by [-sent,-recv]",
                 "events_per_gpu": a.events, "keys_per_gpu": a.keys, "zipf_s": a.zipf, "topk": a.topk,
                 "groups_per_gpu": c2["groups_per_gpu"],
-                "parallelism": f"ingest-partitioned x{world}, RCCL all-gather top-K merge",
+                "parallelism": (f"ingest-partitioned x{world}, all-gather top-K merge over "
+                                + ("igx_dist_* (RCCL, C ABI)" if transport == "igx" else
+                                   "torch.distributed (nccl = RCCL)")) if world > 1 else "single GPU",
             },
             "roofline": c2["roofline"],
             "cpu_baseline": c2.get("cpu_baseline"),

@@ -106,6 +106,15 @@ typedef struct {
     uint32_t negate;
     uint32_t ref_len; /* valid bytes in ref */
     uint8_t ref[IGX_MAX_REF];
+    /* Group-by predicates only: a guard restricts the test to the rows whose guard column
+     * (guard_col, an integer column of guard_len = 1/2/4/8 bytes) equals guard_ref; the other
+     * rows pass.  A BPF program with one probe per event kind checks some fields on one kind
+     * only, e.g. top tcp's receive probe drops `copied <= 0` (tcptop.bpf.c:124-130) while the
+     * send probe has no such check (:112-116): {col = size as int32, GT 0, guard dir == 1}.
+     * guard_len 0 = unguarded (what igx_filter_parse emits; igx_filter rejects guards). */
+    uint32_t guard_col;
+    uint32_t guard_len;
+    uint8_t guard_ref[8];
 } igx_pred;
 
 /* One sort key as Prepare emits it, in sortBy order (first = highest priority). */
@@ -290,6 +299,17 @@ int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t ncols,
                           uint64_t base_idx);
 /* Synchronises; fills the view; IGX_ENOSPC if capacity was exceeded. */
 int igx_groupby_finalize(igx_table *t, igx_table_view *view);
+/* Diagnostics: the form the current interval runs in and AUTO's plan for the next ones. */
+typedef struct {
+    uint32_t form;       /* IGX_GB_CACHED / IGX_GB_DIRECT / IGX_GB_PART (0 before the interval's first update) */
+    uint32_t region;     /* 1: the interval's partitioned updates run the region variant */
+    uint32_t part_left;  /* AUTO: intervals still planned in the partitioned form */
+    uint32_t exact_left; /* AUTO: intervals partitioned exactly after a region overflowed */
+    uint32_t sm_probers; /* the cached form's probers: 1 state machine, 0 batch */
+    uint32_t pad;
+    uint64_t rows;       /* rows fed to the interval so far */
+} igx_groupby_info_t;
+int igx_groupby_info(igx_table *t, igx_groupby_info_t *out);
 /* igx_groupby_finalize without its host synchronisation: the occupied-slot list is built on
  * the device and the group count stays there (view->d_n_groups; view->n_groups is 0 until
  * igx_groupby_wait).  igx_groupby_sort's top-K of such a table (0 < k <= 4096, no float or
@@ -298,7 +318,9 @@ int igx_groupby_finalize(igx_table *t, igx_table_view *view);
  * tracer.go:177-226, with no wait in it).  The count and the status igx_groupby_finalize
  * would have returned (IGX_ENOSPC) come back from igx_groupby_wait, or from the first
  * igx_groupby_reset / igx_groupby_finalize that finds the read-back landed (a reset never
- * waits for the device).  The read-back is written by the kernel that counts the groups into
+ * waits for the device), or, when the next interval's igx_groupby_finalize_async collects it,
+ * from that call (which still issues its own interval; the error text names the failed
+ * finalize) -- igx_groupby_wait only ever reports the last finalize's own status.  The read-back is written by the kernel that counts the groups into
  * the table's coherent pinned buffer, followed by a sequence number the host polls (no copy
  * and no event on the stream); igx_groupby_wait polls it, and fails with IGX_EIO if the
  * stream drains without it.  Asynchronous. */
@@ -412,6 +434,10 @@ int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int rank, igx_dis
 int igx_dist_destroy(igx_dist *d);
 int igx_dist_rank(igx_dist *d, int *rank, int *nranks);
 int igx_dist_barrier(igx_dist *d);   /* synchronises */
+/* Marks the communicator unusable, as a failed group does: every later call returns IGX_EIO
+ * without entering a collective.  For a caller that learned of a peer's failure out of band
+ * (e.g. a node's gRPC stream ended, grpc-runtime.go:221-237). */
+int igx_dist_mark_broken(igx_dist *d);
 /* C3: in-place sum of a u32 buffer (log2 histograms) over all ranks (mod 2^32, exact).  Async. */
 int igx_dist_allreduce_u32(igx_dist *d, uint32_t *buf, uint64_t n);
 /* Top-K candidate merge (C2, C5): every rank's nrows x row_bytes rows (device) concatenated in

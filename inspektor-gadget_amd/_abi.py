@@ -38,12 +38,19 @@ class Col(C.Structure):
 
 class Pred(C.Structure):
     _fields_ = [("col", C.c_uint32), ("cmp", C.c_uint32), ("negate", C.c_uint32),
-                ("ref_len", C.c_uint32), ("ref", C.c_uint8 * MAX_REF)]
+                ("ref_len", C.c_uint32), ("ref", C.c_uint8 * MAX_REF),
+                ("guard_col", C.c_uint32), ("guard_len", C.c_uint32), ("guard_ref", C.c_uint8 * 8)]
 
 
 class SortKey(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("width", C.c_uint32), ("kind", C.c_uint32),
                 ("desc", C.c_uint32), ("col", C.c_uint32)]
+
+
+class GroupbyInfo(C.Structure):
+    _fields_ = [("form", C.c_uint32), ("region", C.c_uint32), ("part_left", C.c_uint32),
+                ("exact_left", C.c_uint32), ("sm_probers", C.c_uint32), ("pad", C.c_uint32),
+                ("rows", C.c_uint64)]
 
 
 class Agg(C.Structure):
@@ -129,6 +136,7 @@ SIGNATURES = [
     ("igx_groupby_finalize", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_finalize_async", _I, [_VP, C.POINTER(TableView)]),
     ("igx_groupby_wait", _I, [_VP, C.POINTER(C.c_uint64)]),
+    ("igx_groupby_info", _I, [_VP, C.POINTER(GroupbyInfo)]),
     ("igx_groupby_gather", _I, [_VP, _VP, _U64, _VP]),
     ("igx_groupby_sort", _I, [_VP, C.POINTER(TSortKey), _U32, _U32, _VP]),
     ("igx_segment_fsum", _I, [_VP, _VP, _U32, _U32, _VP, _U64, _VP, _VP, _U32, _VP]),
@@ -147,6 +155,7 @@ SIGNATURES = [
     ("igx_dist_destroy", _I, [_VP]),
     ("igx_dist_rank", _I, [_VP, C.POINTER(_I), C.POINTER(_I)]),
     ("igx_dist_barrier", _I, [_VP]),
+    ("igx_dist_mark_broken", _I, [_VP]),
     ("igx_dist_allreduce_u32", _I, [_VP, _VP, _U64]),
     ("igx_dist_allgather_rows", _I, [_VP, _VP, _U64, _U32, _VP, _U64, C.POINTER(_U64)]),
     ("igx_dist_alltoallv_rows", _I, [_VP, _VP, C.POINTER(_U64), _U32, _VP, _U64, C.POINTER(_U64)]),

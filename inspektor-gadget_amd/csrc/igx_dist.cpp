@@ -33,6 +33,17 @@ struct igx_dist {
     uint64_t *d_cnt = nullptr;    // exchange_groups: rows per owner
 };
 
+// a group's end: when it fails, the peers' matching sends / receives may never complete, so
+// the communicator is marked unusable (later calls fail with IGX_EIO before any collective)
+#define IGX_NCCL_END(d)                                                                     \
+    do {                                                                                    \
+        ncclResult_t r_ = ncclGroupEnd();                                                   \
+        if (r_ != ncclSuccess) {                                                            \
+            (d)->broken = true;                                                             \
+            return igx_fail((d)->ctx, IGX_EIO, "ncclGroupEnd: %s", ncclGetErrorString(r_)); \
+        }                                                                                   \
+    } while (0)
+
 // the widest per-rank meta row any call gathers: alltoallv's send counts, capacity, flags
 static constexpr size_t META_WORDS = IGX_DIST_MAX_RANKS + 2;
 
@@ -143,19 +154,20 @@ extern "C" int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int ra
     d->nranks = nranks;
     // the metadata buffers are sized once here, so no collective ever allocates (an
     // allocation failure on one rank would leave the others waiting in the all-gather)
-    if (hipMalloc(&d->d_meta, META_WORDS * (nranks + 1) * 8) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&d->h_meta), META_WORDS * (nranks + 1) * 8, hipHostMallocDefault) !=
-            hipSuccess) {
-        (void)hipFree(d->d_meta);
-        delete d;
-        return igx_fail(ctx, IGX_ENOMEM, "dist_init: metadata buffers");
-    }
+    const bool mem_ok =
+        hipMalloc(&d->d_meta, META_WORDS * (nranks + 1) * 8) == hipSuccess &&
+        hipHostMalloc(reinterpret_cast<void **>(&d->h_meta), META_WORDS * (nranks + 1) * 8, hipHostMallocDefault) ==
+            hipSuccess;
     d->meta_words = META_WORDS;
+    // every rank joins the communicator's creation, even one whose allocation failed: the
+    // peers' ncclCommInitRank waits for all ranks; a failed rank then aborts its side
     const ncclResult_t r = ncclCommInitRank(&d->comm, nranks, uid, rank);
-    if (r != ncclSuccess) {
+    if (r != ncclSuccess || !mem_ok) {
+        if (r == ncclSuccess) (void)ncclCommAbort(d->comm);
         (void)hipFree(d->d_meta);
         (void)hipHostFree(d->h_meta);
         delete d;
+        if (!mem_ok) return igx_fail(ctx, IGX_ENOMEM, "dist_init: metadata buffers");
         return igx_fail(ctx, IGX_EIO, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
     }
     *out = d;
@@ -171,6 +183,12 @@ extern "C" int igx_dist_destroy(igx_dist *d) {
     (void)hipFree(d->part);
     (void)hipFree(d->d_cnt);
     delete d;
+    return IGX_OK;
+}
+
+extern "C" int igx_dist_mark_broken(igx_dist *d) {
+    if (!d) return IGX_EINVAL;
+    d->broken = true;
     return IGX_OK;
 }
 
@@ -206,11 +224,24 @@ static int plan_fail(igx_dist *d, const igx_dist_plan &p, const char *what) {
 
 extern "C" int igx_dist_allreduce_u32(igx_dist *d, uint32_t *buf, uint64_t n) {
     if (!d) return IGX_EINVAL;
+    if (d->broken) return igx_fail(d->ctx, IGX_EIO, "dist: communicator broken by an earlier failure");
     if (n == 0) return IGX_OK;
-    if (!buf) return igx_fail(d->ctx, IGX_EINVAL, "dist_allreduce: null buffer");
+    if (!buf) {
+        // the peers are already in (or will enter) the all-reduce of n words: take part with
+        // zeros so they complete, then fail this rank's call
+        void *z = nullptr;
+        if (igx_scratch(d->ctx, n * 4, &z) || hipMemsetAsync(z, 0, n * 4, d->ctx->stream) != hipSuccess ||
+            ncclAllReduce(z, z, n, ncclUint32, ncclSum, d->comm, d->ctx->stream) != ncclSuccess)
+            d->broken = true;
+        return igx_fail(d->ctx, IGX_EINVAL, "dist_allreduce: null buffer");
+    }
     // u32 addition mod 2^32 is exact and order-independent: the merged histogram equals the
     // histogram of the union of every rank's events
-    IGX_NCCL(d, ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, d->comm, d->ctx->stream));
+    const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, d->comm, d->ctx->stream);
+    if (r != ncclSuccess) {
+        d->broken = true;
+        return igx_fail(d->ctx, IGX_EIO, "ncclAllReduce: %s", ncclGetErrorString(r));
+    }
     return IGX_OK;
 }
 
@@ -248,7 +279,7 @@ extern "C" int igx_dist_allgather_rows(igx_dist *d, const void *rows, uint64_t n
             IGX_NCCL_G(d, ncclRecv(o + p.recv_off[q] * row_bytes, p.recv_counts[q] * row_bytes, ncclUint8, q, d->comm,
                                    ctx->stream));
     }
-    IGX_NCCL(d, ncclGroupEnd());
+    IGX_NCCL_END(d);
     return IGX_OK;
 }
 
@@ -283,7 +314,7 @@ extern "C" int igx_dist_alltoallv_rows(igx_dist *d, const void *rows, const uint
         if (sc) IGX_NCCL_G(d, ncclSend(s + p.send_off[q] * row_bytes, sc * row_bytes, ncclUint8, q, d->comm, ctx->stream));
         if (rcv) IGX_NCCL_G(d, ncclRecv(o + p.recv_off[q] * row_bytes, rcv * row_bytes, ncclUint8, q, d->comm, ctx->stream));
     }
-    IGX_NCCL(d, ncclGroupEnd());
+    IGX_NCCL_END(d);
     return IGX_OK;
 }
 

@@ -453,6 +453,22 @@ extern "C" int igx_regex_compile_blob(const char *pattern, size_t len, uint8_t *
     return IGX_OK;
 }
 
+int igx_check_guard(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred &p) {
+    if (p.guard_col >= ncols) return igx_fail(ctx, IGX_EINVAL, "predicate guard column %u out of range", p.guard_col);
+    const igx_col &g = cols[p.guard_col];
+    if (g.kind != IGX_KIND_INT && g.kind != IGX_KIND_UINT)
+        return igx_fail(ctx, IGX_EINVAL, "predicate guard on a non-integer column");
+    if (p.guard_len != g.width || (g.width != 1 && g.width != 2 && g.width != 4 && g.width != 8))
+        return igx_fail(ctx, IGX_EINVAL, "predicate guard of %u bytes on a %u-byte column", p.guard_len, g.width);
+    return IGX_OK;
+}
+
+uint64_t igx_guard_ref(const igx_pred &p) {
+    uint64_t r = 0;
+    for (uint32_t b = 0; b < p.guard_len && b < 8; ++b) r |= (uint64_t)p.guard_ref[b] << (8 * b);
+    return r;
+}
+
 int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                     uint32_t npreds, DevPreds *out) {
     std::memset(out, 0, sizeof *out);
@@ -483,6 +499,13 @@ int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx
         if (c.kind == IGX_KIND_FLOAT && c.width != 4 && c.width != 8)
             return igx_fail(ctx, IGX_EINVAL, "float column width %u", c.width);
         std::memcpy(d.ref, p.ref, IGX_MAX_REF);
+        if (p.guard_len) {
+            int rc = igx_check_guard(ctx, cols, ncols, p);
+            if (rc) return rc;
+            d.gptr = static_cast<const uint8_t *>(cols[p.guard_col].ptr);
+            d.gwidth = p.guard_len;
+            d.gref = igx_guard_ref(p);
+        }
     }
     out->n = npreds;
     return IGX_OK;
@@ -497,6 +520,8 @@ static int filter_chunked(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, con
     if (!out_n || (nrows && !out_idx)) return igx_fail(ctx, IGX_EINVAL, "filter: null output");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "filter: more than 2^32 rows");
     if (npreds && !preds) return igx_fail(ctx, IGX_EINVAL, "filter: null predicates");
+    for (uint32_t i = 0; i < npreds; ++i)
+        if (preds[i].guard_len) return igx_fail(ctx, IGX_EINVAL, "filter: guarded predicates are group-by only");
     const uint32_t nchunks = npreds ? (npreds + IGX_KMAX_PREDS - 1) / IGX_KMAX_PREDS : 1;
     std::vector<DevPreds> dps(nchunks);
     for (uint32_t c = 0; c < nchunks; ++c) {

@@ -57,6 +57,9 @@ struct DevPred {
     uint32_t width, kind, cmp, negate;
     uint32_t ref_len, pad;
     const uint8_t *dfa;   // IGX_CMP_REGEX: device regex automaton (igx_regex.h blob)
+    const uint8_t *gptr;  // guard column (igx_pred.guard_*): the test applies where it equals gref
+    uint64_t gref;
+    uint32_t gwidth, gpad;   // gwidth 0: unguarded
     uint8_t ref[IGX_MAX_REF];
 };
 struct DevPreds {
@@ -65,6 +68,9 @@ struct DevPreds {
 };
 int igx_build_preds(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred *preds,
                     uint32_t npreds, DevPreds *out);
+// a predicate's guard (igx_pred.guard_*): validated against the columns; its value as u64
+int igx_check_guard(igx_ctx *ctx, const igx_col *cols, uint32_t ncols, const igx_pred &p);
+uint64_t igx_guard_ref(const igx_pred &p);
 
 // ---------------------------------------------------------------------------------
 // launchers (defined in the k_*.hip files)

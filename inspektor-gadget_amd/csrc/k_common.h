@@ -155,6 +155,11 @@ __device__ __forceinline__ bool regex_match(const uint8_t *blob, const uint8_t *
 
 // getComparisonFuncForComparisonType (filter.go:236-263): (field OP ref) != negate
 __device__ __forceinline__ bool pred_match(const DevPred &d, uint64_t row) {
+    if (d.gwidth) {   // guarded (group-by only): rows of another kind pass
+        uint64_t g = 0;
+        for (uint32_t b = 0; b < d.gwidth; ++b) g |= (uint64_t)d.gptr[row * d.gwidth + b] << (8 * b);
+        if (g != d.gref) return true;
+    }
     if (d.cmp == IGX_CMP_REGEX) return regex_match(d.dfa, d.ptr + row * d.width, d.width) != (d.negate != 0);
     int c = pred_cmp(d, row);
     bool r;

@@ -39,7 +39,9 @@
 // cache is committed with HBM atomics at the end.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -111,10 +113,16 @@ struct GbArgs {
     // offset of the high dword (4 for 8-byte columns, else 0)
     uint32_t vldw[AMAX], cldw[AMAX], vhioff[AMAX], chioff[AMAX], phioff[PMAX], validw;
     uint32_t naggs;
-    // scalar predicates (FilterSpec on a <= 8-byte column), AND-ed
+    // scalar predicates (FilterSpec on a <= 8-byte column), AND-ed.  pldw: load stride (0 when
+    // pshare < AMAX: the column is aggregate pshare's value column, whose raw value is reused).
+    // A guarded predicate applies to the rows whose guard column equals gref; the fused
+    // kernels read the guard as aggregate pguard's condition value (a guard on any other
+    // column goes to the row mask), the mask kernel loads it from gptr (gwidth bytes).
     const uint8_t *pptr[PMAX];
-    uint64_t pref[PMAX];
+    const uint8_t *gptr[PMAX];
+    uint64_t pref[PMAX], gref[PMAX];
     uint32_t pwidth[PMAX], pkind[PMAX], pcmp[PMAX], pneg[PMAX], pcnt[PMAX];
+    uint32_t pldw[PMAX], pshare[PMAX], pguard[PMAX], gwidth[PMAX];
     uint32_t npred;
     uint32_t lds_entries;   // E (8 x sets)
     uint32_t direct;        // 1: probers issue their HBM atomics; the server wave probes too
@@ -527,7 +535,7 @@ __device__ __forceinline__ void issue_row(const GbArgs &a, uint64_t row, RowRaw<
     R.vraw = ldd(a.validp, row * a.validw);
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
-        const uint64_t b = row * a.pwidth[p];
+        const uint64_t b = row * a.pldw[p];
         R.plo[p] = ldd(a.pptr[p], b);
         R.phi[p] = ldd(a.pptr[p], b + a.phioff[p]);
     }
@@ -591,8 +599,15 @@ __device__ __forceinline__ bool row_raw(const GbArgs &a, uint64_t row, const Row
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
         if (p < (int)a.npred) {
-            const uint64_t pv = assemble(R.plo[p], R.phi[p], row * a.pwidth[p], a.pwidth[p]);
-            ok = ok && pred_scalar(pv, a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p], a.pcnt[p]);
+            uint64_t pv = assemble(R.plo[p], R.phi[p], row * a.pwidth[p], a.pwidth[p]);
+#pragma unroll
+            for (int x = 0; x < NA; ++x)
+                if (a.pshare[p] == (uint32_t)x) pv = rv[x];
+            bool r = pred_scalar(pv, a.pref[p], a.pwidth[p], a.pkind[p], a.pcmp[p], a.pneg[p], a.pcnt[p]);
+#pragma unroll
+            for (int x = 0; x < NA; ++x)
+                if (a.pguard[p] == (uint32_t)x) r = r || rc[x] != a.gref[p];
+            ok = ok && r;
         }
     }
     return ok;
@@ -1542,6 +1557,13 @@ struct igx_table {
     uint64_t fin_seq = 0;           // the last finalize's number (fin_host[3] once it has landed)
     bool fin_pending = false;       // igx_groupby_finalize_async not yet collected
     int fin_status = 0;             // status of a collected asynchronous finalize, not yet returned
+    uint64_t fin_status_seq = 0;    // ... and the finalize it belongs to
+    // the finalized interval's own bookkeeping, taken when its finalize is issued: the read-back
+    // may be collected after the next interval's reset and updates changed the live fields
+    struct {
+        uint64_t rows_fed;
+        bool direct, part, region;
+    } fin_snap{};
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[32] = {};      // IP text of the groups, per IGX_TSRC_IPTEXT sort key
     uint64_t text_rows[32] = {};
@@ -2166,14 +2188,26 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     // more predicates, regex or string rules -- are AND-ed into a row mask first by a scan
     // with the filter's predicate evaluator (k_common.h), which then masks rows like `valid`.
     std::vector<igx_pred> fused, masked;
+    // a guard is fused when it is the condition column of an aggregate (whose raw value the
+    // kernel holds anyway): that aggregate's index, else AMAX
+    auto guard_agg = [&](const igx_pred &q) -> uint32_t {
+        const igx_col &g = cols[q.guard_col];
+        for (uint32_t x = 0; x < t->naggs; ++x)
+            if (a.hascond[x] && a.cptr[x] == static_cast<const uint8_t *>(g.ptr) && a.cwidth[x] == g.width) return x;
+        return AMAX;
+    };
     auto fusable = [&](const igx_pred &q) {
         const igx_col &c = cols[q.col];
         return !(q.cmp == IGX_CMP_REGEX || c.kind == IGX_KIND_BYTES || c.kind == IGX_KIND_BOOL ||
                  c.kind == IGX_KIND_OTHER || (c.width != 1 && c.width != 2 && c.width != 4 && c.width != 8) ||
-                 (c.kind == IGX_KIND_FLOAT && c.width < 4));
+                 (c.kind == IGX_KIND_FLOAT && c.width < 4) || (q.guard_len && guard_agg(q) == AMAX));
     };
     for (uint32_t p = 0; p < npreds; ++p) {
         if (preds[p].col >= ncols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: predicate column out of range");
+        if (preds[p].guard_len) {
+            const int rc = igx_check_guard(ctx, cols, ncols, preds[p]);
+            if (rc) return rc;
+        }
         (fusable(preds[p]) ? fused : masked).push_back(preds[p]);
     }
     while (fused.size() > PMAX) {   // overflow into the mask, set tests (IN) last: the mask scan has none
@@ -2221,10 +2255,25 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         const uint32_t nb = q.cmp == IGX_CMP_IN ? q.ref_len : c.width;
         for (uint32_t b = 0; b < nb; ++b) r |= (uint64_t)q.ref[b] << (8 * b);
         a.pref[p] = r;
+        a.pldw[p] = c.width;
+        a.pshare[p] = a.pguard[p] = AMAX;
+        for (uint32_t x = 0; x < t->naggs; ++x)   // the value column of an aggregate: reuse its load
+            if (a.pshare[p] == AMAX && !a.vcount[x] && a.vptr[x] == a.pptr[p] && a.vwidth[x] == c.width) {
+                a.pshare[p] = x;
+                a.pldw[p] = 0;
+            }
+        a.gptr[p] = dummy;
+        if (q.guard_len) {
+            a.pguard[p] = guard_agg(q);
+            a.gptr[p] = static_cast<const uint8_t *>(cols[q.guard_col].ptr);
+            a.gwidth[p] = q.guard_len;
+            a.gref[p] = igx_guard_ref(q);
+        }
     }
     for (uint32_t p = npreds; p < PMAX; ++p) {
-        a.pptr[p] = dummy;
-        a.pwidth[p] = 0;
+        a.pptr[p] = a.gptr[p] = dummy;
+        a.pwidth[p] = a.pldw[p] = 0;
+        a.pshare[p] = a.pguard[p] = AMAX;
     }
     for (uint32_t p = 0; p < PMAX; ++p) a.phioff[p] = a.pwidth[p] == 8 ? 4 : 0;
     a.npred = npreds;
@@ -2326,6 +2375,10 @@ static int fin_launch(igx_table *t) {
                        t->tile_cnt);
     // the kernel that finds the group count also writes the read-back into fin_host
     const uint64_t seq = ++t->fin_seq;
+    t->fin_snap.rows_fed = t->rows_fed;
+    t->fin_snap.direct = t->interval_direct;
+    t->fin_snap.part = t->interval_part;
+    t->fin_snap.region = t->interval_region;
     if (tiles <= SLOTS_INLINE_TILES) {
         hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                            (const uint32_t *)nullptr, t->tile_cnt, t->groups, t->n_groups, t->err, t->fin_dev, seq);
@@ -2363,16 +2416,17 @@ static int fin_apply(igx_table *t) {
     const uint64_t misses = h[1];
     const uint64_t ng = h[2];
     const uint32_t spilled = reinterpret_cast<const uint32_t *>(h)[1];   // a region overflowed
-    if (spilled && t->interval_region) t->region_off = DIRECT_RUN + 1;
+    const auto &f = t->fin_snap;   // the interval this read-back belongs to
+    if (spilled && f.region) t->region_off = DIRECT_RUN + 1;
     t->host_groups = ng;
     // Miss-heavy streams (most rows miss the LDS cache: near-uniform, high-cardinality keys)
     // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When
     // nearly every row missed, the cache is pure overhead: AUTO runs the next DIRECT_RUN
     // intervals in the partitioned form (streamed passes instead of a random HBM probe per
     // row; C4: 4.1 vs 4.4 ms direct, 6.4 ms cached), then one cached interval to measure again.
-    if (t->rows_fed >= 1000000 && !t->interval_direct && !t->interval_part) {
-        t->prefer_sm = misses * 10 > t->rows_fed * 7;
-        if (t->mode == IGX_GB_AUTO && misses * 100 > t->rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
+    if (f.rows_fed >= 1000000 && !f.direct && !f.part) {
+        t->prefer_sm = misses * 10 > f.rows_fed * 7;
+        if (t->mode == IGX_GB_AUTO && misses * 100 > f.rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }
     if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
     if (ng > t->cap)
@@ -2397,7 +2451,10 @@ static int fin_collect(igx_table *t, uint64_t *n_groups) {
             std::this_thread::yield();
         }
         const int rc = fin_apply(t);
-        if (rc && !t->fin_status) t->fin_status = rc;
+        if (rc && !t->fin_status) {
+            t->fin_status = rc;
+            t->fin_status_seq = t->fin_seq;
+        }
     }
     if (n_groups) *n_groups = t->host_groups;
     return t->fin_status;
@@ -2420,19 +2477,44 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
 extern "C" int igx_groupby_finalize_async(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    (void)fin_collect(t, nullptr);   // the previous one landed long ago (it precedes this interval)
+    // the previous interval's read-back (it precedes this interval) is collected first; a
+    // failure of that interval comes back from this call -- after this interval is issued,
+    // so the caller's pipeline stays intact -- and igx_groupby_wait reports this one's only
+    (void)fin_collect(t, nullptr);
+    const int earlier = t->fin_status;
+    const uint64_t earlier_seq = t->fin_status_seq;
+    t->fin_status = IGX_OK;
     const int rc = fin_launch(t);
     if (rc) return rc;
     t->fin_pending = true;
     fin_view(t, view, 0);
+    if (earlier) {
+        const std::string why = igx_last_error(ctx);   // the collected interval's message
+        return igx_fail(ctx, earlier, "groupby: the previous interval (finalize %llu) failed: %s",
+                        (unsigned long long)earlier_seq, why.c_str());
+    }
     return IGX_OK;
 }
 
 extern "C" int igx_groupby_wait(igx_table *t, uint64_t *n_groups) {
     if (!t) return IGX_EINVAL;
-    const int rc = fin_collect(t, n_groups);
+    int rc = fin_collect(t, n_groups);
+    if (rc && t->fin_status_seq != t->fin_seq) rc = IGX_OK;   // an older interval's (never reached here)
     t->fin_status = IGX_OK;
     return rc;
+}
+
+extern "C" int igx_groupby_info(igx_table *t, igx_groupby_info_t *out) {
+    if (!t || !out) return IGX_EINVAL;
+    std::memset(out, 0, sizeof *out);
+    if (t->rows_fed)
+        out->form = t->interval_part ? IGX_GB_PART : (t->interval_direct ? IGX_GB_DIRECT : IGX_GB_CACHED);
+    out->region = t->interval_part && t->interval_region ? 1u : 0u;
+    out->part_left = t->direct_left;
+    out->exact_left = t->region_off;
+    out->sm_probers = t->prefer_sm ? 1u : 0u;
+    out->rows = t->rows_fed;
+    return IGX_OK;
 }
 
 extern "C" int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows) {

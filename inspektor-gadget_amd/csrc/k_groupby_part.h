@@ -219,8 +219,9 @@ __global__ __launch_bounds__(256) void k_gbp_mask(GbArgs a, uint8_t *out) {
     for (uint64_t row = (uint64_t)blockIdx.x * 256 + threadIdx.x; row < a.n; row += (uint64_t)gridDim.x * 256) {
         bool ok = !a.valid || a.valid[row] != 0;
         for (uint32_t q = 0; q < a.npred && q < PMAX; ++q)
-            ok = ok && pred_scalar(ld_val(a.pptr[q], row, a.pwidth[q]), a.pref[q], a.pwidth[q], a.pkind[q], a.pcmp[q],
-                                   a.pneg[q], a.pcnt[q]);
+            ok = ok && ((a.gwidth[q] && ld_val(a.gptr[q], row, a.gwidth[q]) != a.gref[q]) ||
+                        pred_scalar(ld_val(a.pptr[q], row, a.pwidth[q]), a.pref[q], a.pwidth[q], a.pkind[q],
+                                    a.pcmp[q], a.pneg[q], a.pcnt[q]));
         out[row] = ok ? 1 : 0;
     }
 }

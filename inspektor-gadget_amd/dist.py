@@ -160,12 +160,12 @@ class IgxComm:
 
 
 def comm():
-    """The transport for the current process group (None without one).  Default: torch's own
-    collectives on the group (on an "nccl" group these are RCCL over xGMI too); IGX_DIST=igx
-    selects the igx_dist_* C ABI on an nccl group.  The C-ABI exchanges' planning
-    (igx_dist_plan_*) is tested for 2..8 ranks against gloo (tests/test_dist_plan.py), but
-    their RCCL send/recv loops have only run with one rank (no multi-GPU box so far), so
-    they stay opt-in until a world >= 2 run on GPUs has checked them."""
+    """The transport for the current process group (None without one): the one
+    select_transport() agreed on, else torch's own collectives (on an "nccl" group these are
+    RCCL over xGMI too), or the igx_dist_* C ABI when IGX_DIST=igx on an nccl group.
+    bench.py selects the C ABI at N > 1 (select_transport("igx")); the library's default stays
+    torch's collectives until a world >= 2 run on GPUs has checked the C ABI's send/recv loops
+    (their planning, igx_dist_plan_*, is tested for 2..8 ranks against gloo)."""
     global _comm
     d = _dist()
     if d is None or d.get_world_size() == 1:
@@ -174,6 +174,33 @@ def comm():
         use_igx = d.get_backend() == "nccl" and os.environ.get("IGX_DIST", "torch") == "igx"
         _comm = IgxComm(d) if use_igx else TorchComm(d)
     return _comm
+
+
+def select_transport(prefer="igx"):
+    """Pick the transport every rank will use, agreed over the process group: prefer="igx"
+    tries the igx_dist_* C ABI (RCCL) on an "nccl" group; if any rank's igx_dist_init fails,
+    every rank falls back to torch's collectives.  Returns the transport's name ("igx" or
+    "torch"), or None without a multi-rank group."""
+    global _comm
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        return None
+    shutdown()
+    c, ok = None, 1
+    if prefer == "igx" and d.get_backend() == "nccl":
+        try:
+            c = IgxComm(d)
+        except Exception:   # noqa: BLE001 -- any local failure: agree on the fallback below
+            c, ok = None, 0
+        torch = torch_mod()
+        flag = torch.tensor([ok], dtype=torch.int32,
+                            device=torch.device("cuda", torch.cuda.current_device()))
+        d.all_reduce(flag, op=d.ReduceOp.MIN)
+        if int(flag.item()) == 0 and c is not None:
+            c.close()
+            c = None
+    _comm = c if c is not None else TorchComm(d)
+    return _comm.name
 
 
 def shutdown():

@@ -232,6 +232,13 @@ class Table:
             self.fin["n_groups"] = n.value
         return n.value
 
+    def info(self):
+        """igx_groupby_info: the current interval's form and AUTO's plan, as a dict."""
+        from ._abi import GroupbyInfo
+        v = GroupbyInfo()
+        self.ctx.check(self.ctx.L.igx_groupby_info(self.h, C.byref(v)))
+        return {f: getattr(v, f) for f, _ in GroupbyInfo._fields_ if f != "pad"}
+
     def reset(self):
         self.ctx.check(self.ctx.L.igx_groupby_reset(self.h))
 

@@ -78,11 +78,18 @@ class Event:
     Stats: list = field(default_factory=list)
 
 
-def _pred(col, cmp, ref_bytes, negate=0):
+def _pred(col, cmp, ref_bytes, negate=0, guard=None):
+    """igx_pred; guard = (column, value bytes): the test applies only where that column
+    holds that value (a check one probe makes and another does not)."""
     p = _abi.Pred()
     p.col, p.cmp, p.negate, p.ref_len = col, cmp, negate, len(ref_bytes)
     for i, x in enumerate(ref_bytes):
         p.ref[i] = x
+    if guard is not None:
+        p.guard_col, gref = guard
+        p.guard_len = len(gref)
+        for i, x in enumerate(gref):
+            p.guard_ref[i] = x
     return p
 
 
@@ -93,6 +100,8 @@ class _TopTracer:
       AGGS       [(kind, value column | None, cond column | None, cond value, out width, divisor)]
       STATS_COLS Columns of the Stats struct (what sortBy names refer to)
       SORT_SRC   Stats column -> ("agg", i) | ("key", field) | ("const",)
+      ALIASES    [(name, event column, torch dtype)]: the column's memory read as another type
+                 (appended after EVENT, e.g. an argument the probe declares signed)
       SortByDefault
     and _preds() (the probe's filters) and _stats(rows) (Stats objects)."""
 
@@ -101,12 +110,15 @@ class _TopTracer:
     AGGS: list = []
     SORT_SRC: Dict[str, tuple] = {}
     SortByDefault: list = []
+    ALIASES: list = []
 
     def __init__(self, MaxRows=_top.MaxRowsDefault, SortBy=None, capacity=1 << 20, Interval=1, ctx=None):
         self.MaxRows = MaxRows
         self.SortBy = list(self.SortByDefault if SortBy is None else SortBy)
         self.Interval = Interval
         self.ev_index = {name: i for i, (name, _, _) in enumerate(self.EVENT)}
+        for j, (name, _, _) in enumerate(self.ALIASES):
+            self.ev_index[name] = len(self.EVENT) + j
         self.ev_width = {name: w for name, _, w in self.EVENT}
         widths = [self.ev_width[k] for k in self.KEY]
         aggs = []
@@ -140,6 +152,8 @@ class _TopTracer:
                 # that no aggregate uses) still need a readable pointer
                 t = torch.zeros(max(1, n), dtype=torch.uint8, device=events[self.KEY[0]].device)
             cols.append(t)
+        for _, src, dtype in self.ALIASES:
+            cols.append(cols[self.ev_index[src]].view(getattr(torch, dtype)))
         self.table.update(cols, [self.ev_index[k] for k in self.KEY], n, base, self._preds())
         self.batches.append((base, n, events))
         self.next_idx = base + n
@@ -269,6 +283,12 @@ class TcpStats:
     FirstIndex: int = 0      # canonical pre-sort position (not in the reference struct)
 
 
+def copied_pred(copied_col, dir_col):
+    """ig_toptcp_clean's `if (copied <= 0) return 0;` (tcptop.bpf.c:124-130) as a group-by
+    predicate: `copied > 0` (int32) on the rows with dir == 1 (tcp_cleanup_rbuf); sends pass."""
+    return _pred(copied_col, _abi.CMP_GT, (0).to_bytes(4, "little"), guard=(dir_col, b"\x01"))
+
+
 class TopTcpTracer(_TopTracer):
     """top tcp: probe_ip keyed by ip_key_t, sent/received += size."""
     EVENT = [("saddr", "bytes", 16), ("daddr", "bytes", 16), ("mntns", "uint", 8), ("pid", "uint", 4),
@@ -277,6 +297,8 @@ class TopTcpTracer(_TopTracer):
     KEY = ["saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family"]
     # dir 0 = tcp_sendmsg (sent), 1 = tcp_cleanup_rbuf (received)
     AGGS = [(_abi.AGG_SUM, "size", "dir", 0, 8, 0), (_abi.AGG_SUM, "size", "dir", 1, 8, 0)]
+    # the receive probe's argument is `int copied` (tcptop.bpf.c:125)
+    ALIASES = [("copied", "size", "int32")]
     STATS_COLS = _stats_columns([("pid", "int32"), ("comm", "string", 16), ("ip", "uint16"),
                                  ("saddr", "string", 46), ("daddr", "string", 46), ("sport", "uint16"),
                                  ("dport", "uint16"), ("sent", "uint64"), ("recv", "uint64")],
@@ -294,14 +316,16 @@ class TopTcpTracer(_TopTracer):
 
     def _preds(self):
         """tcptop.bpf.c:42-55: target_pid (0 = all), target_family (-1 = all), then the
-        probe drops every family but AF_INET / AF_INET6."""
+        probe drops every family but AF_INET / AF_INET6; before any of it the receive probe
+        returns when `copied <= 0` (tcptop.bpf.c:124-130; sends have no such check)."""
         fam, pid = self.ev_index["family"], self.ev_index["pid"]
+        recv_pos = copied_pred(self.ev_index["copied"], self.ev_index["dir"])
         inet = _pred(fam, _abi.CMP_IN, AF_INET.to_bytes(2, "little") + AF_INET6.to_bytes(2, "little"))
         if self.TargetFamily not in (-1, AF_INET, AF_INET6):
             # an impossible family: the two tests contradict, no event is kept
             return [_pred(fam, _abi.CMP_EQ, (self.TargetFamily & 0xFFFF).to_bytes(2, "little")), inet]
         preds = [inet if self.TargetFamily == -1 else
-                 _pred(fam, _abi.CMP_EQ, self.TargetFamily.to_bytes(2, "little"))]
+                 _pred(fam, _abi.CMP_EQ, self.TargetFamily.to_bytes(2, "little")), recv_pos]
         if self.TargetPid:
             preds.append(_pred(pid, _abi.CMP_EQ, (self.TargetPid & 0xFFFFFFFF).to_bytes(4, "little")))
         return preds

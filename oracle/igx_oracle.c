@@ -555,6 +555,10 @@ u64 or_top_tcp(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 *pi
     u64 *first = (u64 *)malloc(maxG * 8);
     ip_key_t key;
     for (u64 i = 0; i < n; i++) {
+        /* ig_toptcp_clean (tcp_cleanup_rbuf, int copied): `if (copied <= 0) return 0;`
+         * before probe_ip, tcptop.bpf.c:124-130; sends have no such check (:112-116), so a
+         * zero-size send still creates its group */
+        if (dir[i] == 1 && (int32_t)size[i] <= 0) continue;
         if (family[i] != 2 && family[i] != 10) continue;   /* tcptop.bpf.c:54-55 */
         memset(&key, 0, sizeof key);
         memcpy(key.saddr, saddr + 16 * i, 16);
@@ -615,6 +619,8 @@ struct mt_job {
     const u64 *mntns;
     const u32 *pid;
     const u16 *lport, *dport, *family;
+    const u32 *tcp_size;  /* top tcp: the receive probe's `copied <= 0` drop (with tcp_dir) */
+    const u8 *tcp_dir;
     const u8 *valid;
     const or_agg *aggs;
     u32 naggs;
@@ -682,6 +688,7 @@ static inline void mt_key(const mt_job *J, u64 i, u8 *buf) {
 
 static inline int mt_keep(const mt_job *J, u64 i) {
     if (J->valid && !J->valid[i]) return 0;
+    if (J->tcp_dir && J->tcp_dir[i] == 1 && (int32_t)J->tcp_size[i] <= 0) return 0;   /* tcptop.bpf.c:127-128 */
     if (J->family && J->family[i] != 2 && J->family[i] != 10) return 0;   /* tcptop.bpf.c:54-55 */
     return 1;
 }
@@ -900,6 +907,7 @@ u64 or_top_tcp_mt(const u8 *saddr, const u8 *daddr, const u64 *mntns, const u32 
     memset(&J, 0, sizeof J);
     J.saddr = saddr; J.daddr = daddr; J.mntns = mntns; J.pid = pid; J.comm = comm;
     J.lport = lport; J.dport = dport; J.family = family;
+    J.tcp_size = size; J.tcp_dir = dir;
     J.aggs = aggs; J.naggs = 2; J.n = n; J.base_idx = base_idx; J.T = nthreads;
     J.sort_agg = sa; J.sort_desc = sd; J.nsort = 2; J.k = k;
     J.want_csum = out_csum != NULL;

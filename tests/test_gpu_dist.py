@@ -88,5 +88,12 @@ def test_igx_dist_rccl_single_rank(igx, torch, oracle):
         torch.cuda.synchronize()
         assert got.value == 1000 and torch.equal(out3, rows)   # one rank owns every key, order kept
         ctx.check(L.igx_dist_barrier(h))
+        # a broken communicator: every call fails with IGX_EIO before entering a collective,
+        # the all-reduce included
+        ctx.check(L.igx_dist_mark_broken(h))
+        assert L.igx_dist_allreduce_u32(h, C.c_void_p(hist.data_ptr()), hist.numel()) == A.IGX_EIO
+        assert L.igx_dist_allgather_rows(h, C.c_void_p(rows.data_ptr()), 1000, 96, None, 0, cnt) == A.IGX_EIO
+        assert L.igx_dist_alltoallv_rows(h, C.c_void_p(rows.data_ptr()), sc, 96, None, 0, rc) == A.IGX_EIO
+        assert L.igx_dist_barrier(h) == A.IGX_EIO
     finally:
         ctx.check(L.igx_dist_destroy(h))

@@ -22,10 +22,10 @@ def test_c2_full_size_table_and_topk(oracle, igx, torch):
     bench = importlib.import_module("bench")
     cdf = E.zipf_cdf(G, 1.1)
     ev = E.gen_tcp(0xC2, 0, G, H.to_device(cdf), 0, N)
-    cols = [ev[k] for k in bench.TCP_NAMES]
+    cols = [ev[k] for k in bench.TCP_NAMES] + [ev["size"].view(torch.int32)]
     tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2], [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)],
                   G + G // 4)
-    tab.update(cols, list(range(8)), N, 0, [bench.family_in_pred(A, 7)])
+    tab.update(cols, list(range(8)), N, 0, [bench.family_in_pred(A, 7), bench.copied_pred(A, 10, 9)])
     fin = tab.finalize()
     top = H.host(tab.gather(tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K)))
     rows = H.host(bench.table_rows(E, torch, tab, fin))

@@ -56,7 +56,7 @@ def test_top_tcp_tracer(oracle, igx, torch, G, target_pid, target_family):
     tr.feed({k: v[half:] for k, v in ev.items()})
     evt = tr.NextEvent()
     fam, pid = ev_h["family"], ev_h["pid"]
-    keep = ((fam == 2) | (fam == 10))
+    keep = ((fam == 2) | (fam == 10)) & ~((ev_h["dir"] == 1) & (ev_h["size"].view(np.int32) <= 0))
     if target_family != -1:
         keep &= fam == target_family
     if target_pid:
@@ -79,6 +79,63 @@ def test_top_tcp_tracer(oracle, igx, torch, G, target_pid, target_family):
     # the interval is drained: the next tick is empty
     assert tr.NextEvent().Stats == []
     tr.destroy()
+
+
+@pytest.mark.parametrize("target_pid", [0, 4242])
+def test_top_tcp_receive_copied_drop(oracle, igx, torch, G, target_pid):
+    """ig_toptcp_clean returns before probe_ip when `int copied <= 0` (tcptop.bpf.c:124-130);
+    the send probe has no such check (:112-116), so a zero-size send still creates its group.
+    The stream holds zero and negative (int32) receives, zero-size sends, and keys whose only
+    events are dropped receives (those groups must not exist).  Through TopTcpTracer (the
+    guarded predicate fused into the cached kernel, and with target_pid a third predicate,
+    so one of them runs as a row mask) and every group-by form, against the oracle's
+    or_top_tcp / or_top_tcp_mt, which restate the drop."""
+    H = igx.columns
+    Gk, n = 4000, 400_000
+    ev_h = oracle.gen_tcp(0xC2, 3, Gk, oracle.zipf_cdf(Gk, 1.1), 0, n)
+    rng = np.random.default_rng(11)
+    size = ev_h["size"]
+    r = rng.integers(0, 8, n)
+    size[r == 0] = 0                                                    # copied == 0 / size 0
+    size[r == 1] = np.uint32(0x80000000) | size[r == 1]                 # negative as int32
+    size[r == 2] = np.uint32(0xFFFFFFFF)                                # -1
+    size[r == 3] = np.uint32(0x7FFFFFFF)                                # INT_MAX: kept
+    # keys seen only through dropped receives: rows of a fresh pid, all dir 1 with copied <= 0
+    lone = rng.choice(n, 300, replace=False)
+    ev_h["pid"][lone] = np.uint32(7_000_000) + np.arange(300, dtype=np.uint32)
+    ev_h["dir"][lone] = 1
+    size[lone] = 0
+    if target_pid:
+        ev_h["pid"][::3] = target_pid
+    ev = _dev(H, ev_h)
+    dir_, s32 = ev_h["dir"], size.view(np.int32)
+    assert ((dir_ == 1) & (s32 <= 0)).sum() > 1000 and ((dir_ == 0) & (size == 0)).sum() > 1000
+    keep = ~((dir_ == 1) & (s32 <= 0))
+    if target_pid:
+        keep &= ev_h["pid"] == target_pid
+    names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family")
+    Gn, keys, aggs, first = _ref_top(
+        oracle, {k: ev_h[k] for k in names},
+        [{"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 0},
+         {"kind": "sum", "val": ev_h["size"], "cond": ev_h["dir"], "cond_val": 1}],
+        keep & ((ev_h["family"] == 2) | (ev_h["family"] == 10)),
+        [(_agg_col(0), "uint64", True), (_agg_col(1), "uint64", True)], 20)
+    if not target_pid:   # the C restatements carry the drop themselves
+        Gc, _, csent, crecv, cfirst = oracle.top_tcp(ev_h, 20)
+        Gm, msent, mrecv, mfirst = oracle.top_tcp_mt(ev_h, 20, threads=4)
+        assert Gc == Gm == Gn
+        assert list(cfirst) == list(mfirst) == [int(x) for x in first]
+        assert list(csent) == list(msent) == aggs[0].tolist() and list(crecv) == aggs[1].tolist()
+    A = igx._abi
+    for mode in (A.GB_AUTO, A.GB_CACHED, A.GB_DIRECT, A.GB_PART):
+        tr = G.TopTcpTracer(TargetPid=target_pid, MaxRows=20, capacity=2 * Gk)
+        tr.table.set_mode(mode)
+        tr.feed(ev)
+        evt = tr.NextEvent()
+        assert tr.table.fin["n_groups"] == Gn, mode
+        assert [s.FirstIndex for s in evt.Stats] == [int(x) for x in first], mode
+        assert [(s.Sent, s.Received) for s in evt.Stats] == list(zip(aggs[0].tolist(), aggs[1].tolist())), mode
+        tr.destroy()
 
 
 def test_top_tcp_sort_by_key_columns(oracle, igx, torch, G):

@@ -311,6 +311,30 @@ def test_async_finalize_device_count_topk(oracle, E, H, igx, torch):
     with pytest.raises(A.IgxError) as ei:
         small.wait()
     assert ei.value.code == A.IGX_ENOSPC
+    # an overflowing interval followed by a clean one with no wait in between: the overflow is
+    # reported once -- by the reset that collects it, or else by the next finalize_async
+    # (which still issues its own interval) -- and wait() reports the clean interval's own
+    # status and count
+    few = int(np.unique(ev_h["pid"][:2000]).size)
+    assert few < 1000
+    for _ in range(3):
+        small.reset()
+        small.update([ev["pid"]], [0], n, 0)                  # overflows
+        small.finalize(sync=False)
+        raised = 0
+        try:
+            small.reset()
+        except A.IgxError as e:
+            assert e.code == A.IGX_ENOSPC
+            raised += 1
+        small.update([ev["pid"][:2000]], [0], 2000, 0)
+        try:
+            small.finalize(sync=False)
+        except A.IgxError as e:
+            assert e.code == A.IGX_ENOSPC and "previous interval" in str(e)
+            raised += 1
+        assert raised == 1
+        assert small.wait() == few
     small.destroy()
 
 

@@ -127,3 +127,40 @@ def test_auto_region_overflow_then_exact(E, H, igx):
         assert row[:4].view(np.uint32)[0] == 0 and row[o:o + 8].view(np.uint64)[0] == cnt[0], it
         assert row[o + 8:o + 16].view(np.uint64)[0] == first[0], it
     tab.destroy()
+
+
+def test_auto_region_overflow_async_pipeline(E, H, igx):
+    """The same stream as test_auto_region_overflow_then_exact, every interval issued without a
+    host synchronisation (reset, update, finalize_async, top-1, gather; the count is waited for
+    only after the next interval is issued).  The region variant's overflow must still switch
+    AUTO to the exact variant within the next two intervals (its read-back is applied with
+    its own interval's bookkeeping), and every interval's hot-key row stays exact."""
+    A = igx._abi
+    rng = np.random.default_rng(5)
+    n = 4_000_000
+    keys = rng.integers(1, 20_000_000, n, dtype=np.uint32)
+    keys[rng.random(n) < 0.05] = 0
+    uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
+    kd = H.to_device(keys)
+    tab = E.Table([4], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], 8_000_000)
+    forms, rows = [], []
+    for it in range(7):
+        tab.reset()
+        tab.update([kd], [0], n, 0)
+        forms.append(tab.info())
+        fin = tab.finalize(sync=False)
+        rows.append(tab.gather(tab.sort([(A.TSRC_AGG, 0, True)], 1)))
+    assert tab.wait() == len(uk)
+    o = fin["key_bytes"]
+    for it, r in enumerate(rows):
+        row = H.host(r)[0]
+        assert row[:4].view(np.uint32)[0] == 0 and row[o:o + 8].view(np.uint64)[0] == cnt[0], it
+        assert row[o + 8:o + 16].view(np.uint64)[0] == first[0], it
+    assert forms[0]["form"] == A.GB_CACHED
+    region = [i for i, f in enumerate(forms) if f["form"] == A.GB_PART and f["region"]]
+    assert region, forms
+    r0 = region[0]
+    later = forms[r0 + 1:r0 + 4]
+    assert any(f["form"] == A.GB_PART and not f["region"] for f in later), forms
+    tab.destroy()
+
