@@ -364,16 +364,66 @@ template <int KW, int NA>
 __device__ __forceinline__ void hbm_merge(const GbArgs &a, const uint32_t (&k)[KW], uint64_t h,
                                           const uint64_t (&v)[NA], uint64_t first);
 
-// a staged record that found its region full: merged into the table directly (exact, slow;
-// never on a hashed stream whose buckets stay within 1.25x their share)
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// Staged records that found their region full are merged into the table directly (exact;
+// never on a hashed stream whose buckets stay within 1.25x their share).  The whole wave
+// calls it, `spill` marks the lanes holding such a record.  A region overflows when one key
+// is hot (its bucket receives its share many times over), so the spilled records of a wave
+// are mostly that key's: they are pre-combined across the wave first (wave64 ballot +
+// shuffle: every distinct key's sums and minimum first index reduced onto its lowest lane),
+// and only the leaders merge -- one record's atomics per key per wave instead of per row.
 template <int KW>
-__device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p, const uint32_t *rec) {
+__device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p, bool spill, const uint32_t *rec) {
+    const uint64_t any = __ballot(spill);
+    if (!any) return;
+    const uint32_t lane = threadIdx.x & 63;
     // err block word 1: a region overflowed this interval (AUTO then partitions exactly)
-    if (!*reinterpret_cast<volatile const uint32_t *>(a.err + 1)) *reinterpret_cast<volatile uint32_t *>(a.err + 1) = 1u;
+    if ((int)lane == __ffsll((long long)any) - 1 && !*reinterpret_cast<volatile const uint32_t *>(a.err + 1))
+        *reinterpret_cast<volatile uint32_t *>(a.err + 1) = 1u;
     uint32_t k[KW];
-    uint64_t v[AMAX], gidx;
-    lds_decode<KW, AMAX>(a, p, rec, k, v, gidx);
-    hbm_merge<KW, AMAX>(a, k, hash_key<KW>(k), v, gidx);
+    uint64_t v[AMAX], gidx = ~0ull;
+#pragma unroll
+    for (int w = 0; w < KW; ++w) k[w] = 0;
+#pragma unroll
+    for (int x = 0; x < AMAX; ++x) v[x] = 0;
+    if (spill) lds_decode<KW, AMAX>(a, p, rec, k, v, gidx);
+    const uint64_t h = hash_key<KW>(k);
+    bool lead = spill;
+    for (uint64_t todo = any; todo;) {   // one round per distinct key among the spilled lanes
+        const int L = __ffsll((long long)todo) - 1;
+        bool same = ((todo >> lane) & 1ull) && h == __shfl((unsigned long long)h, L);
+        if (__ballot(same) != (1ull << L)) {
+#pragma unroll
+            for (int w = 0; w < KW; ++w) same = same && k[w] == __shfl(k[w], L);
+        }
+        const uint64_t peers = __ballot(same);
+        todo &= ~peers;
+        if (__popcll(peers) < 2) continue;
+#pragma unroll
+        for (int x = 0; x < AMAX; ++x) {
+            if (x < (int)a.naggs) {
+                const unsigned long long t = wave_sum_u64(same ? (unsigned long long)v[x] : 0ull);
+                if ((int)lane == L) v[x] = t;
+            }
+        }
+        const unsigned long long f = wave_min_u64(same ? (unsigned long long)gidx : ~0ull);
+        if ((int)lane == L) gidx = f;
+        else if (same) lead = false;
+    }
+    if (lead) hbm_merge<KW, AMAX>(a, k, h, v, gidx);
 }
 
 // ---- A: a tile of rows -> records, each first-level bucket's run at its exact position -----
@@ -435,13 +485,19 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     if (p.dbg & 1u) return;
     uint4 *out = reinterpret_cast<uint4 *>(p.recs1);
     const uint32_t nq = total * rq;
-    for (uint32_t qi = threadIdx.x; qi < nq; qi += PTA) {
+    // every lane of a wave runs the same number of iterations (the spill path is wave-wide)
+    for (uint32_t q0 = threadIdx.x & ~63u; q0 < nq; q0 += PTA) {
+        const uint32_t qi = q0 + (threadIdx.x & 63);
+        const bool live = qi < nq;
         const uint32_t j = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
-        const uint32_t q = qi - j * rq, b = sb[j];
+        const uint32_t q = qi - j * rq, b = live ? sb[j] : 0u;
         const uint32_t g = base[b] + j - off[b];
-        if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
+        bool spill = false;
+        if (!live) {
+        } else if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
         else if (g < p.reg1) out[((uint64_t)b * p.reg1 + g) * rq + q] = stage[qi];
-        else if (q == 0) region_spill<KW>(a, p, reinterpret_cast<const uint32_t *>(stage + (uint64_t)j * rq));
+        else spill = q == 0;
+        if (p.reg1) region_spill<KW>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? j : 0u) * rq));
     }
 }
 
@@ -551,14 +607,19 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     __syncthreads();
     if (p.dbg & 4u) return;
     uint4 *out = reinterpret_cast<uint4 *>(p.recs2);
-    for (uint32_t qi = threadIdx.x; qi < nq; qi += PTA) {
+    for (uint32_t q0 = threadIdx.x & ~63u; q0 < nq; q0 += PTA) {   // wave-uniform trip count
+        const uint32_t qi = q0 + (threadIdx.x & 63);
+        const bool live = qi < nq;
         const uint32_t jj = rq == 1 ? qi : __umulhi(qi, p.rq_magic);   // sorted position
         const uint32_t q = qi - jj * rq;
-        const uint32_t sidx = perm[jj], b = bkt[sidx];
+        const uint32_t sidx = live ? perm[jj] : 0u, b = bkt[sidx];
         const uint32_t g = base[b] + jj - off[b];
-        if (!p.reg2) out[(uint64_t)g * rq + q] = stage[sidx * rq + q];
+        bool spill = false;
+        if (!live) {
+        } else if (!p.reg2) out[(uint64_t)g * rq + q] = stage[sidx * rq + q];
         else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * rq + q] = stage[sidx * rq + q];
-        else if (q == 0) region_spill<KW>(a, p, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
+        else spill = q == 0;
+        if (p.reg2) region_spill<KW>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
     }
 }
 
@@ -709,19 +770,6 @@ __device__ __forceinline__ void flush_owned(const GbArgs &a, const AggTab<KW> &T
     atomicOr(a.err, 4u);
 }
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(x, o);
-        x = y < x ? y : x;
-    }
-    return x;
-}
 
 // Wave64 pre-combine (a whole wave calls it): the lowest lane still to be merged leads; the
 // lanes holding the same key (hash, then every key word, compared with the leader's) hand

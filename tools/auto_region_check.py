@@ -1,7 +1,12 @@
 """Diagnostics: AUTO on a miss-heavy stream with one hot key (5% of the rows).  Interval 1
 runs cached and measures the misses, interval 2 the partitioned region variant (the hot
 key's bucket overflows its region), later ones the exact variant.  Prints ms per interval
-and checks every interval's group count against numpy."""
+and checks every interval's group count against numpy.
+
+  python tools/auto_region_check.py            AUTO
+  IGX_GB_MODE=1 python tools/auto_region_check.py                       cached every interval
+  IGX_GB_MODE=3 IGX_GBP_REGION=1 python tools/auto_region_check.py      interval 0: region variant
+                                                                        with overflow, then exact"""
 import importlib
 import os
 import sys

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 __device__ __forceinline__ uint64_t mix(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -47,10 +48,10 @@ __global__ void k_probe(const uint4 *tab, uint64_t nrec, uint64_t per, uint32_t 
     if (acc == 0x12345678u) sink[0] = 1;
 }
 
-int main() {
+int main(int argc, char **argv) {
     uint4 *tab;
     uint32_t *sink;
-    const uint64_t bytes = 256ull << 20;
+    const uint64_t bytes = (argc > 1 ? strtoull(argv[1], nullptr, 0) : 256ull) << 20;
     hipMalloc(&tab, bytes);
     hipMemset(tab, 1, bytes);
     hipMalloc(&sink, 64);
