@@ -916,10 +916,9 @@ __device__ __forceinline__ void miss_push(const MissRing<KW, NA> &m, const uint3
     __hip_atomic_store(sq, p + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Probers resolve PB misses per lane at a time: the LDS cache again (a prober may have
-// adopted the key since), then all PB HBM probes are issued before the first is waited
-// for, then each is finished: adoption of a free LDS entry, or the HBM-update ring.
-constexpr int PB = 1;   // 2 was measured slower (register spills, bigger batches)
+// Probers resolve one miss per lane at a time (two per lane were measured slower: register
+// spills, bigger batches): the LDS cache again (a prober may have adopted the key since), then
+// the HBM table, then adoption of a free LDS entry or the HBM-update ring.
 
 template <int KW, int NA>
 struct MissRow {
@@ -1112,72 +1111,208 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
     }
 }
 
+// Cooperative claim stores (the whole wave calls it; `claim` marks the lanes that won a
+// slot's tag this round).  A claimer's key record (key words, padding, tag) and value record
+// (first = its event index, its own values) are spread over the wave -- lane l writes quad
+// l % CQ of the (l / CQ)-th claim of the round -- so each record leaves as one store
+// instruction's adjacent 16-B pieces: one write-through request per 64 B, instead of a request
+// per 16-B store of a lane writing its record alone (C5: 5 of a claim's 8 requests, C2: 7 of 10).
+// Ends with s_waitcnt vmcnt(0): the records are visible before the claimers publish `ready`.
+template <int KW, int NA>
+__device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, uint32_t s, const uint32_t (&k)[KW],
+                                                 uint64_t tag, uint64_t gidx, const uint64_t (&v)[NA]) {
+    constexpr uint32_t KOFF = koff_of(KW);
+    constexpr int KQ = (int)((KOFF + 8) / 16);   // key quads, through the tag word when it ends one
+    constexpr int VQ = (NA + 2) / 2;             // first + NA aggregates
+    constexpr int CQ = KQ + VQ;
+    constexpr uint32_t RPI = 64 / CQ;            // claims per store instruction
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t w[CQ * 4];
+#pragma unroll
+    for (int i = 0; i < KQ * 4; ++i) {
+        const uint32_t b = 4u * (uint32_t)i;
+        w[i] = b < 4u * KW ? k[i] : (b < KOFF ? 0u : (b == KOFF ? (uint32_t)tag : (uint32_t)(tag >> 32)));
+    }
+#pragma unroll
+    for (int i = 0; i < VQ * 2; ++i) {
+        const uint64_t x = i == 0 ? gidx : (i - 1 < NA && (uint32_t)(i - 1) < a.naggs ? v[i - 1 < NA ? i - 1 : 0] : 0ull);
+        w[KQ * 4 + 2 * i] = (uint32_t)x;
+        w[KQ * 4 + 2 * i + 1] = (uint32_t)(x >> 32);
+    }
+    const uint32_t r = lane / CQ, q = lane % CQ;
+    const __amdgpu_buffer_rsrc_t rk = rec_rsrc(a);
+    for (uint64_t todo = __ballot(claim); todo;) {
+        uint64_t m = todo;
+        for (uint32_t i = 0; i < r && m; ++i) m &= m - 1;   // the r-th claimer of the round
+        const bool mine = r < RPI && m != 0;
+        const uint32_t src = mine ? (uint32_t)__ffsll((long long)m) - 1 : lane;
+        const uint32_t slot = __shfl(s, (int)src);
+        uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int qq = 0; qq < CQ; ++qq) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t y = __shfl(w[4 * qq + j], (int)src);
+                if (q == (uint32_t)qq) o[j] = y;
+            }
+        }
+        if (mine) {
+            const u4v val = {o[0], o[1], o[2], o[3]};
+            if (q < (uint32_t)KQ) {
+                __builtin_amdgcn_raw_buffer_store_b128(val, rk, slot * a.krec_len + 16 * q, 0, 16 /* sc1 */);
+            } else {
+                const uint32_t off = 16 * (q - KQ), vlen = a.vrec_words * 8;
+                uint64_t *vr = a.vrec + (uint64_t)slot * a.vrec_words;
+                if (off + 16 <= vlen) {
+                    if (a.vrec_total) {
+                        const __amdgpu_buffer_rsrc_t rv =
+                            __builtin_amdgcn_make_buffer_rsrc(a.vrec, (short)0, (int)a.vrec_total, 0x00020000);
+                        __builtin_amdgcn_raw_buffer_store_b128(val, rv, slot * a.vrec_words * 8 + off, 0, 16 /* sc1 */);
+                    } else {
+                        st_agent(vr + off / 8, (uint64_t)o[0] | ((uint64_t)o[1] << 32));
+                        st_agent(vr + off / 8 + 1, (uint64_t)o[2] | ((uint64_t)o[3] << 32));
+                    }
+                } else if (off < vlen) {
+                    st_agent(vr + off / 8, (uint64_t)o[0] | ((uint64_t)o[1] << 32));
+                }
+            }
+        }
+        for (uint32_t i = 0; i < RPI && todo; ++i) todo &= todo - 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The batch prober: a wave takes 64 cells of the miss ring and resolves them together, one
+// round trip per round: every unresolved lane reads its current slot's record; a lane that
+// finds it empty claims it (CAS), and the round's claims are written cooperatively
+// (claim_store_coop) and published before the next round.  A lane that meets its own tag
+// not yet published -- possibly claimed by a lane of this very wave -- reads it again next
+// round instead of spinning.  Resolved misses then adopt a free LDS entry or go to the
+// HBM-update ring.
 template <int KW, int NA, bool DBG>
 __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
                                        const MissRing<KW, NA> &m, uint32_t lane) {
+    constexpr uint32_t KOFF = koff_of(KW);
+    constexpr int NQ = probe_quads<KW>();
+    const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     for (;;) {
         uint32_t claim = 0;
-        if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u * PB);
+        if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u);
         claim = __shfl(claim, 0);
-        bool have[PB];
-        MissRow<KW, NA> x[PB];
-#pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            const uint32_t p = claim + lane + 64u * j;
+        MissRow<KW, NA> x;
+        bool have = true;
+        {
+            const uint32_t p = claim + lane;
             uint32_t *sq = &m.seq[p % MRING];
-            have[j] = true;
             uint32_t spins = 0;
             while (__hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p + 1) {
                 if (__hip_atomic_load(&m.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == a.nl) {
                     if (p >= __hip_atomic_load(&m.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                        have[j] = false;   // past the last miss of a finished stream
+                        have = false;   // past the last miss of a finished stream
                         break;
                     }
                     // the loaders are done, so the cell is being written right now: bounded
-                    if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have[j] = false; break; }
+                    if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have = false; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);   // waiting for misses: as long as the stream lasts
                 if (DBG && m.waits) atomicAdd(m.waits + 5, 1ull);              // prober: ring empty
             }
-            if (have[j]) {
-                read_cell<KW, NA>(m, p, x[j]);
+            if (have) {
+                read_cell<KW, NA>(m, p, x);
                 __hip_atomic_store(sq, p + MRING, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // free
             }
         }
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < PB; ++j) any = any || have[j];
-        if (__ballot(any) == 0) break;
-        if (DBG && (a.dbg & 1024u)) continue;   // diagnostics: hand-off only (cells taken, dropped)
-        bool probe[PB];
-        uint32_t d[PB][probe_quads<KW>() * 4];
-#pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            probe[j] = false;
-            if (have[j]) {
-                uint32_t gs = SLOT_OVF;
-                const int slot = lds_lookup<KW>(c, x[j].k, x[j].h, gs);
-                if (slot >= 0) lds_accumulate<KW, NA>(a, c, slot, x[j].v, x[j].gidx);
-                else probe[j] = true;
-            }
+        if (__ballot(have) == 0) break;
+        bool act = false;
+        if (have) {
+            uint32_t gs = SLOT_OVF;
+            const int slot = lds_lookup<KW>(c, x.k, x.h, gs);
+            if (slot >= 0) lds_accumulate<KW, NA>(a, c, slot, x.v, x.gidx);
+            else act = true;
         }
-#pragma unroll
-        for (int j = 0; j < PB; ++j)
-            if (probe[j] && !(DBG && (a.dbg & 256u))) probe_issue<KW>(a, x[j].h, d[j]);
-#pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            if (probe[j]) {
-                uint64_t first_ins = 0;
-                uint32_t gs;
-                bool claimed = false;
-                if (DBG && (a.dbg & 256u)) gs = (uint32_t)home_slot(a, x[j].h);   // diagnostics: no probe
-                else gs = find_or_insert<KW, true, NA>(a, x[j].k, x[j].h, x[j].gidx, first_ins, d[j], x[j].v, claimed);
-                if (gs != SLOT_OVF) {
-                    const int ad = ghost_admit<KW>(a, c, x[j].h) ? lds_adopt<KW>(c, x[j].k, x[j].h, gs) : -1;
-                    if (claimed) continue;   // its values are in the new record already
-                    if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x[j].v, x[j].gidx);
-                    else ring_push<NA>(a, r, gs, x[j].v, x[j].gidx, first_ins);
+        uint32_t gs = SLOT_OVF;
+        uint64_t first_ins = 0;
+        bool claimed = false;
+        if (DBG && (a.dbg & 256u) && act) {   // diagnostics: no probe (the home slot, unverified)
+            gs = (uint32_t)home_slot(a, x.h);
+            act = false;
+        }
+        const uint64_t tag = (x.h & ~EP_MAX) | a.ep;
+        uint64_t s = home_slot(a, x.h);
+        uint32_t d[NQ * 4];
+        if (act) load_rec<NQ>(rs, (uint32_t)(s * a.krec_len), d);
+        uint32_t probes = 0, tries = 0;
+        bool reread = false;
+        while (__ballot(act)) {
+            bool won = false;
+            if (act) {
+                uint8_t *rec = a.krec + s * a.krec_len;
+                uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
+                uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
+                bool next = false;
+                if ((t & EP_MAX) != a.ep) {   // empty in this interval: claim it
+                    if (x.gidx >= READY_IDX) {   // an index column value that `ready` cannot carry
+                        atomicOr(a.err, 8u);
+                        act = false;
+                    } else {
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(rec + KOFF),
+                                                       (unsigned long long)t, (unsigned long long)tag);
+                        if (old == t) {
+                            won = true;
+                            act = false;
+                            gs = (uint32_t)s;
+                        } else {
+                            t = old;     // a claim raced ours: its key may still be in flight
+                            ready = 0;
+                        }
+                    }
                 }
+                if (act) {
+                    if (t == tag) {
+                        if (!ready_ok(ready, a.ep)) {
+                            if (++tries > (1u << 22)) { atomicOr(a.err, 2u); act = false; }   // read again
+                        } else {
+                            bool eq = true;
+#pragma unroll
+                            for (int w = 0; w < KW; ++w) eq = eq && (d[w] == x.k[w]);
+                            if (eq) {
+                                gs = (uint32_t)s;
+                                first_ins = (ready & READY_IDX) - 1;
+                                act = false;
+                            } else if (!reread) {
+                                // the quads of one snapshot are separate loads: `ready` may have
+                                // been sampled after the key quads, so read the record once more
+                                reread = true;
+                            } else {
+                                next = true;
+                            }
+                        }
+                    } else {
+                        next = true;
+                    }
+                }
+                if (next) {
+                    reread = false;
+                    s = next_slot(a, s);
+                    if (++probes >= a.max_probe) { atomicOr(a.err, 4u); act = false; }
+                }
+            }
+            if (__ballot(won)) {
+                claim_store_coop<KW, NA>(a, won, (uint32_t)s, x.k, tag, x.gidx, x.v);
+                if (won) {
+                    st_agent(reinterpret_cast<uint64_t *>(a.krec + s * a.krec_len + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
+                    atomicOr(a.occ + (s >> 5), 1u << (s & 31));
+                    first_ins = x.gidx;
+                    claimed = true;
+                }
+            }
+            if (act) load_rec<NQ>(rs, (uint32_t)(s * a.krec_len), d);
+        }
+        if (gs != SLOT_OVF) {
+            const int ad = ghost_admit<KW>(a, c, x.h) ? lds_adopt<KW>(c, x.k, x.h, gs) : -1;
+            if (!claimed) {   // a claim's values are in its new record already
+                if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x.v, x.gidx);
+                else ring_push<NA>(a, r, gs, x.v, x.gidx, first_ins);
             }
         }
     }
