@@ -916,8 +916,8 @@ __device__ __forceinline__ void miss_push(const MissRing<KW, NA> &m, const uint3
     __hip_atomic_store(sq, p + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Probers resolve one miss per lane at a time (two per lane were measured slower: register
-// spills, bigger batches): the LDS cache again (a prober may have adopted the key since), then
+// Probers resolve PB misses per lane at a time (PB = 1: two per lane measured slower -- C5
+// 6.41 -> 6.72-6.80 ms, C2 unchanged, and for the 72-B key they spill): the LDS cache again (a prober may have adopted the key since), then
 // the HBM table, then adoption of a free LDS entry or the HBM-update ring.
 
 template <int KW, int NA>
@@ -1189,7 +1189,7 @@ __device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, ui
 // not yet published -- possibly claimed by a lane of this very wave -- reads it again next
 // round instead of spinning.  Resolved misses then adopt a free LDS entry or go to the
 // HBM-update ring.
-template <int KW, int NA, bool DBG>
+template <int KW, int NA, bool DBG, int PB>
 __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
                                        const MissRing<KW, NA> &m, uint32_t lane) {
     constexpr uint32_t KOFF = koff_of(KW);
@@ -1197,123 +1197,145 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
     for (;;) {
         uint32_t claim = 0;
-        if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u);
+        if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u * PB);
         claim = __shfl(claim, 0);
-        MissRow<KW, NA> x;
-        bool have = true;
-        {
-            const uint32_t p = claim + lane;
+        MissRow<KW, NA> x[PB];
+        bool have[PB], act[PB];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const uint32_t p = claim + lane + 64u * j;
             uint32_t *sq = &m.seq[p % MRING];
             uint32_t spins = 0;
+            have[j] = true;
             while (__hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p + 1) {
                 if (__hip_atomic_load(&m.ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == a.nl) {
                     if (p >= __hip_atomic_load(&m.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                        have = false;   // past the last miss of a finished stream
+                        have[j] = false;   // past the last miss of a finished stream
                         break;
                     }
                     // the loaders are done, so the cell is being written right now: bounded
-                    if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have = false; break; }
+                    if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); have[j] = false; break; }
                 }
                 __builtin_amdgcn_s_sleep(1);   // waiting for misses: as long as the stream lasts
                 if (DBG && m.waits) atomicAdd(m.waits + 5, 1ull);              // prober: ring empty
             }
-            if (have) {
-                read_cell<KW, NA>(m, p, x);
+            if (have[j]) {
+                read_cell<KW, NA>(m, p, x[j]);
                 __hip_atomic_store(sq, p + MRING, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // free
             }
         }
-        if (__ballot(have) == 0) break;
-        bool act = false;
-        if (have) {
-            uint32_t gs = SLOT_OVF;
-            const int slot = lds_lookup<KW>(c, x.k, x.h, gs);
-            if (slot >= 0) lds_accumulate<KW, NA>(a, c, slot, x.v, x.gidx);
-            else act = true;
-        }
-        uint32_t gs = SLOT_OVF;
-        uint64_t first_ins = 0;
-        bool claimed = false;
-        if (DBG && (a.dbg & 256u) && act) {   // diagnostics: no probe (the home slot, unverified)
-            gs = (uint32_t)home_slot(a, x.h);
-            act = false;
-        }
-        const uint64_t tag = (x.h & ~EP_MAX) | a.ep;
-        uint64_t s = home_slot(a, x.h);
-        uint32_t d[NQ * 4];
-        if (act) load_rec<NQ>(rs, (uint32_t)(s * a.krec_len), d);
-        uint32_t probes = 0, tries = 0;
-        bool reread = false;
-        while (__ballot(act)) {
-            bool won = false;
-            if (act) {
-                uint8_t *rec = a.krec + s * a.krec_len;
-                uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
-                uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
-                bool next = false;
-                if ((t & EP_MAX) != a.ep) {   // empty in this interval: claim it
-                    if (x.gidx >= READY_IDX) {   // an index column value that `ready` cannot carry
-                        atomicOr(a.err, 8u);
-                        act = false;
-                    } else {
-                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(rec + KOFF),
-                                                       (unsigned long long)t, (unsigned long long)tag);
-                        if (old == t) {
-                            won = true;
-                            act = false;
-                            gs = (uint32_t)s;
-                        } else {
-                            t = old;     // a claim raced ours: its key may still be in flight
-                            ready = 0;
-                        }
-                    }
-                }
-                if (act) {
-                    if (t == tag) {
-                        if (!ready_ok(ready, a.ep)) {
-                            if (++tries > (1u << 22)) { atomicOr(a.err, 2u); act = false; }   // read again
-                        } else {
-                            bool eq = true;
+        bool any = false;
 #pragma unroll
-                            for (int w = 0; w < KW; ++w) eq = eq && (d[w] == x.k[w]);
-                            if (eq) {
-                                gs = (uint32_t)s;
-                                first_ins = (ready & READY_IDX) - 1;
-                                act = false;
-                            } else if (!reread) {
-                                // the quads of one snapshot are separate loads: `ready` may have
-                                // been sampled after the key quads, so read the record once more
-                                reread = true;
+        for (int j = 0; j < PB; ++j) any = any || have[j];
+        if (__ballot(any) == 0) break;
+        uint32_t gs[PB];
+        uint64_t first_ins[PB], s[PB];
+        bool claimed[PB], reread[PB];
+        uint32_t probes[PB], tries[PB];
+        uint32_t d[PB][NQ * 4];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            act[j] = false;
+            gs[j] = SLOT_OVF;
+            first_ins[j] = 0;
+            claimed[j] = reread[j] = false;
+            probes[j] = tries[j] = 0;
+            if (have[j]) {
+                uint32_t g = SLOT_OVF;
+                const int slot = lds_lookup<KW>(c, x[j].k, x[j].h, g);
+                if (slot >= 0) lds_accumulate<KW, NA>(a, c, slot, x[j].v, x[j].gidx);
+                else act[j] = true;
+            }
+            if (DBG && (a.dbg & 256u) && act[j]) {   // diagnostics: no probe (the home slot, unverified)
+                gs[j] = (uint32_t)home_slot(a, x[j].h);
+                act[j] = false;
+            }
+            s[j] = home_slot(a, x[j].h);
+            if (act[j]) load_rec<NQ>(rs, (uint32_t)(s[j] * a.krec_len), d[j]);
+        }
+        for (;;) {
+            bool more = false;
+#pragma unroll
+            for (int j = 0; j < PB; ++j) more = more || act[j];
+            if (!__ballot(more)) break;
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                const uint64_t tag = (x[j].h & ~EP_MAX) | a.ep;
+                bool won = false;
+                if (act[j]) {
+                    uint8_t *rec = a.krec + s[j] * a.krec_len;
+                    uint64_t t = (uint64_t)d[j][KOFF / 4] | ((uint64_t)d[j][KOFF / 4 + 1] << 32);
+                    uint64_t ready = (uint64_t)d[j][KOFF / 4 + 2] | ((uint64_t)d[j][KOFF / 4 + 3] << 32);
+                    bool next = false;
+                    if ((t & EP_MAX) != a.ep) {   // empty in this interval: claim it
+                        if (x[j].gidx >= READY_IDX) {   // an index column value that `ready` cannot carry
+                            atomicOr(a.err, 8u);
+                            act[j] = false;
+                        } else {
+                            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(rec + KOFF),
+                                                           (unsigned long long)t, (unsigned long long)tag);
+                            if (old == t) {
+                                won = true;
+                                act[j] = false;
+                                gs[j] = (uint32_t)s[j];
                             } else {
-                                next = true;
+                                t = old;     // a claim raced ours: its key may still be in flight
+                                ready = 0;
                             }
                         }
-                    } else {
-                        next = true;
+                    }
+                    if (act[j]) {
+                        if (t == tag) {
+                            if (!ready_ok(ready, a.ep)) {
+                                if (++tries[j] > (1u << 22)) { atomicOr(a.err, 2u); act[j] = false; }   // read again
+                            } else {
+                                bool eq = true;
+#pragma unroll
+                                for (int w = 0; w < KW; ++w) eq = eq && (d[j][w] == x[j].k[w]);
+                                if (eq) {
+                                    gs[j] = (uint32_t)s[j];
+                                    first_ins[j] = (ready & READY_IDX) - 1;
+                                    act[j] = false;
+                                } else if (!reread[j]) {
+                                    // the quads of one snapshot are separate loads: `ready` may have
+                                    // been sampled after the key quads, so read the record once more
+                                    reread[j] = true;
+                                } else {
+                                    next = true;
+                                }
+                            }
+                        } else {
+                            next = true;
+                        }
+                    }
+                    if (next) {
+                        reread[j] = false;
+                        s[j] = next_slot(a, s[j]);
+                        if (++probes[j] >= a.max_probe) { atomicOr(a.err, 4u); act[j] = false; }
                     }
                 }
-                if (next) {
-                    reread = false;
-                    s = next_slot(a, s);
-                    if (++probes >= a.max_probe) { atomicOr(a.err, 4u); act = false; }
+                if (__ballot(won)) {
+                    claim_store_coop<KW, NA>(a, won, (uint32_t)s[j], x[j].k, tag, x[j].gidx, x[j].v);
+                    if (won) {
+                        st_agent(reinterpret_cast<uint64_t *>(a.krec + s[j] * a.krec_len + KOFF + 8),
+                                 (a.ep << 48) | (x[j].gidx + 1));
+                        atomicOr(a.occ + (s[j] >> 5), 1u << (s[j] & 31));
+                        first_ins[j] = x[j].gidx;
+                        claimed[j] = true;
+                    }
                 }
             }
-            if (__ballot(won)) {
-                claim_store_coop<KW, NA>(a, won, (uint32_t)s, x.k, tag, x.gidx, x.v);
-                if (won) {
-                    st_agent(reinterpret_cast<uint64_t *>(a.krec + s * a.krec_len + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
-                    atomicOr(a.occ + (s >> 5), 1u << (s & 31));
-                    first_ins = x.gidx;
-                    claimed = true;
-                }
-            }
-            if (act) load_rec<NQ>(rs, (uint32_t)(s * a.krec_len), d);
+#pragma unroll
+            for (int j = 0; j < PB; ++j)
+                if (act[j]) load_rec<NQ>(rs, (uint32_t)(s[j] * a.krec_len), d[j]);
         }
-        if (gs != SLOT_OVF) {
-            const int ad = ghost_admit<KW>(a, c, x.h) ? lds_adopt<KW>(c, x.k, x.h, gs) : -1;
-            if (!claimed) {   // a claim's values are in its new record already
-                if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x.v, x.gidx);
-                else ring_push<NA>(a, r, gs, x.v, x.gidx, first_ins);
-            }
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            if (gs[j] == SLOT_OVF) continue;
+            const int ad = ghost_admit<KW>(a, c, x[j].h) ? lds_adopt<KW>(c, x[j].k, x[j].h, gs[j]) : -1;
+            if (claimed[j]) continue;   // a claim's values are in its new record already
+            if (ad >= 0) lds_accumulate<KW, NA>(a, c, ad, x[j].v, x[j].gidx);
+            else ring_push<NA>(a, r, gs[j], x[j].v, x[j].gidx, first_ins[j]);
         }
     }
 }
@@ -1360,7 +1382,7 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
         ring_serve<DBG>(a, r, lane);
     } else if (wave >= a.nl) {
         if (a.sm) prober_sm<KW, NA, DBG>(a, c, r, m, lane);
-        else prober<KW, NA, DBG>(a, c, r, m, lane);
+        else prober<KW, NA, DBG, 1>(a, c, r, m, lane);
         if (lane == 0) atomicAdd(&r.ctl[2], 1u);
     } else {
         const uint32_t PTB = a.nl * 64;   // rows per workgroup step
@@ -2053,9 +2075,9 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     static size_t lds_set[5] = {0, 0, 0, 0, 0};
     const void *kern[5] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_a<L, NV>),
-                           reinterpret_cast<const void *>(k_gbp_b<KW, NV>),
-                           reinterpret_cast<const void *>(k_gbp_c<KW, NV, AMAX>),
-                           reinterpret_cast<const void *>(k_gbp_c<KW, NV, 0>)};
+                           reinterpret_cast<const void *>(k_gbp_b<L, NV>),
+                           reinterpret_cast<const void *>(k_gbp_c<L, NV, AMAX>),
+                           reinterpret_cast<const void *>(k_gbp_c<L, NV, 0>)};
     const size_t need[5] = {lds_k, lds_a, lds_b, t->naggs ? lds_c : 0, t->naggs ? 0 : lds_c};
     for (int i = 0; i < 5; ++i) {
         if (need[i] > lds_set[i]) {
@@ -2069,7 +2091,7 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
         hipLaunchKernelGGL((k_gbp_a<L, NV>), dim3(p.tiles_a), dim3(PTA), lds_a, ctx->stream, a, p);
         if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
         hipLaunchKernelGGL(k_gbr_tiles, dim3(1), dim3(1024), 0, ctx->stream, p);
-        hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
+        hipLaunchKernelGGL((k_gbp_b<L, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
         if (p.dbg & 512u) return IGX_OK;   // ... after pass B
         hipLaunchKernelGGL(k_gbr_items, dim3(1), dim3(1024), 0, ctx->stream, p);
     }
@@ -2083,13 +2105,13 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     if (p.dbg & 1024u) return IGX_OK;   // diagnostics: stop after the count and the scans
     hipLaunchKernelGGL((k_gbp_a<L, NV>), dim3(p.tiles_a), dim3(PTA), lds_a, ctx->stream, a, p);
     if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
-    hipLaunchKernelGGL((k_gbp_b<KW, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
+    hipLaunchKernelGGL((k_gbp_b<L, NV>), dim3((unsigned)tiles_b), dim3(PTA), lds_b, ctx->stream, a, p);
     if (p.dbg & 512u) return IGX_OK;   // ... after pass B
     }
     if (t->naggs)
-        hipLaunchKernelGGL((k_gbp_c<KW, NV, AMAX>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
+        hipLaunchKernelGGL((k_gbp_c<L, NV, AMAX>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     else   // distinct-only (C4): no aggregate decode or accumulate in the per-record path
-        hipLaunchKernelGGL((k_gbp_c<KW, NV, 0>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
+        hipLaunchKernelGGL((k_gbp_c<L, NV, 0>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     return IGX_OK;
 }
 

@@ -147,11 +147,62 @@ __device__ __forceinline__ void prow_stage(const PartArgs &p, uint64_t row, cons
     if (p.iw == 2) rec[p.ipos + 1] = (uint32_t)(R.fi >> 32);
 }
 
+// The record's packed key words (launch_part's rule: 1- and 2-byte columns share words, the
+// others keep theirs), known at compile time for the static key layouts: the passes then
+// decode a record with constant offsets and masks (a record's words come from one or two
+// 16-B LDS reads) instead of per-word descriptors held in registers.
+struct PackTab {
+    uint32_t kpw[KWMAX], ksh[KWMAX], kmsk[KWMAX];
+    uint32_t kpn;
+};
+template <class L>
+__host__ __device__ constexpr PackTab pack_static() {
+    PackTab t{};
+    uint32_t wp = 0, used = 4, shared = 0, w = 0;
+    for (int c = 0; c < L::NC; ++c) {
+        const uint32_t cw = (uint32_t)L::Ws[c];
+        if (cw <= 2) {
+            if (used + cw > 4) {
+                shared = wp++;
+                used = 0;
+            }
+            t.kpw[w] = shared;
+            t.ksh[w] = 8 * used;
+            t.kmsk[w] = cw == 1 ? 0xFFu : 0xFFFFu;
+            used += cw;
+            ++w;
+        } else {
+            for (uint32_t j = 0; j < (cw + 3) / 4; ++j, ++w) {
+                t.kpw[w] = wp++;
+                t.ksh[w] = 0;
+                t.kmsk[w] = 0xFFFFFFFFu;
+            }
+        }
+    }
+    t.kpn = wp;
+    return t;
+}
+template <class L, bool S = L::is_static>
+struct PackKey {
+    static constexpr bool known = false;
+};
+template <class L>
+struct PackKey<L, true> {
+    static constexpr bool known = true;
+    static constexpr PackTab T = pack_static<L>();
+};
+
 // the table's key words back from a record in LDS
-template <int KW>
-__device__ __forceinline__ void lds_key(const PartArgs &p, const uint32_t *rec, uint32_t (&k)[KW]) {
+template <class L>
+__device__ __forceinline__ void lds_key(const PartArgs &p, const uint32_t *rec, uint32_t (&k)[L::KW]) {
+    if constexpr (PackKey<L>::known) {
+        constexpr PackTab T = PackKey<L>::T;
 #pragma unroll
-    for (int j = 0; j < KW; ++j) k[j] = p.kmsk[j] ? (rec[p.kpw[j]] >> p.ksh[j]) & p.kmsk[j] : 0u;
+        for (int j = 0; j < L::KW; ++j) k[j] = T.kmsk[j] ? (rec[T.kpw[j]] >> T.ksh[j]) & T.kmsk[j] : 0u;
+    } else {
+#pragma unroll
+        for (int j = 0; j < L::KW; ++j) k[j] = p.kmsk[j] ? (rec[p.kpw[j]] >> p.ksh[j]) & p.kmsk[j] : 0u;
+    }
 }
 
 __device__ __forceinline__ uint64_t lds_field(const uint32_t *rec, uint32_t pos, uint32_t w2) {
@@ -164,10 +215,10 @@ __device__ __forceinline__ uint64_t lds_field(const uint32_t *rec, uint32_t pos,
 __host__ __device__ constexpr int nax(int na) { return na > 0 ? na : 1; }
 
 // a record in LDS -> key words, the values its aggregates add, its global event index
-template <int KW, int NA>
-__device__ __forceinline__ void lds_decode(const GbArgs &a, const PartArgs &p, const uint32_t *rec, uint32_t (&k)[KW],
+template <class L, int NA>
+__device__ __forceinline__ void lds_decode(const GbArgs &a, const PartArgs &p, const uint32_t *rec, uint32_t (&k)[L::KW],
                                            uint64_t (&v)[nax(NA)], uint64_t &gidx) {
-    lds_key<KW>(p, rec, k);
+    lds_key<L>(p, rec, k);
     v[0] = 0;
     if constexpr (NA > 0) {
         uint64_t rv[NA], rc[NA];
@@ -385,8 +436,9 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x)
 // are mostly that key's: they are pre-combined across the wave first (wave64 ballot +
 // shuffle: every distinct key's sums and minimum first index reduced onto its lowest lane),
 // and only the leaders merge -- one record's atomics per key per wave instead of per row.
-template <int KW>
+template <class L>
 __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p, bool spill, const uint32_t *rec) {
+    constexpr int KW = L::KW;
     const uint64_t any = __ballot(spill);
     if (!any) return;
     const uint32_t lane = threadIdx.x & 63;
@@ -399,15 +451,15 @@ __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p,
     for (int w = 0; w < KW; ++w) k[w] = 0;
 #pragma unroll
     for (int x = 0; x < AMAX; ++x) v[x] = 0;
-    if (spill) lds_decode<KW, AMAX>(a, p, rec, k, v, gidx);
+    if (spill) lds_decode<L, AMAX>(a, p, rec, k, v, gidx);
     const uint64_t h = hash_key<KW>(k);
     bool lead = spill;
     for (uint64_t todo = any; todo;) {   // one round per distinct key among the spilled lanes
-        const int L = __ffsll((long long)todo) - 1;
-        bool same = ((todo >> lane) & 1ull) && h == __shfl((unsigned long long)h, L);
-        if (__ballot(same) != (1ull << L)) {
+        const int ld = __ffsll((long long)todo) - 1;
+        bool same = ((todo >> lane) & 1ull) && h == __shfl((unsigned long long)h, ld);
+        if (__ballot(same) != (1ull << ld)) {
 #pragma unroll
-            for (int w = 0; w < KW; ++w) same = same && k[w] == __shfl(k[w], L);
+            for (int w = 0; w < KW; ++w) same = same && k[w] == __shfl(k[w], ld);
         }
         const uint64_t peers = __ballot(same);
         todo &= ~peers;
@@ -416,11 +468,11 @@ __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p,
         for (int x = 0; x < AMAX; ++x) {
             if (x < (int)a.naggs) {
                 const unsigned long long t = wave_sum_u64(same ? (unsigned long long)v[x] : 0ull);
-                if ((int)lane == L) v[x] = t;
+                if ((int)lane == ld) v[x] = t;
             }
         }
         const unsigned long long f = wave_min_u64(same ? (unsigned long long)gidx : ~0ull);
-        if ((int)lane == L) gidx = f;
+        if ((int)lane == ld) gidx = f;
         else if (same) lead = false;
     }
     if (lead) hbm_merge<KW, AMAX>(a, k, h, v, gidx);
@@ -497,7 +549,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
         } else if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
         else if (g < p.reg1) out[((uint64_t)b * p.reg1 + g) * rq + q] = stage[qi];
         else spill = q == 0;
-        if (p.reg1) region_spill<KW>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? j : 0u) * rq));
+        if (p.reg1) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? j : 0u) * rq));
     }
 }
 
@@ -555,8 +607,9 @@ __global__ __launch_bounds__(1024) void k_gbr_items(PartArgs p) {
 // B tile `blockIdx.x` = records [j * trb, (j + 1) * trb) of first-level bucket b1 in recs1
 // (contiguous): loaded flat into LDS (coalesced), ranked by the next f2 hash bits with LDS
 // atomics, and each final bucket's run written at a cursor reserved with one atomic.
-template <int KW, int NV>
+template <class L, int NV>
 __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
+    constexpr int KW = L::KW;
     constexpr int U = 16;              // quads in flight per thread: a whole tile at once
     extern __shared__ uint8_t lds_raw[];
     const uint32_t tile = blockIdx.x;
@@ -589,7 +642,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += PTA) {
         uint32_t k[KW];
-        lds_key<KW>(p, reinterpret_cast<const uint32_t *>(stage + i * rq), k);
+        lds_key<L>(p, reinterpret_cast<const uint32_t *>(stage + i * rq), k);
         const uint32_t b2 = hash_bits(hash_key<KW>(k), p.f1, p.f2);
         bkt[i] = (uint16_t)b2;
         rank[i] = (uint16_t)atomicAdd(&hist[b2], 1u);
@@ -619,7 +672,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
         } else if (!p.reg2) out[(uint64_t)g * rq + q] = stage[sidx * rq + q];
         else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * rq + q] = stage[sidx * rq + q];
         else spill = q == 0;
-        if (p.reg2) region_spill<KW>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
+        if (p.reg2) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
     }
 }
 
@@ -830,12 +883,13 @@ __device__ __forceinline__ uint64_t lds_hash(const uint32_t (&k)[KW]) {
     return x;
 }
 
-template <int KW, int NA>
-__device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<KW> &T, bool ok,
+template <class L, int NA>
+__device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const AggTab<L::KW> &T, bool ok,
                                       const uint32_t *rec) {
+    constexpr int KW = L::KW;
     uint32_t k[KW];
     uint64_t v[nax(NA)], gidx = 0;
-    lds_decode<KW, NA>(a, p, rec, k, v, gidx);
+    lds_decode<L, NA>(a, p, rec, k, v, gidx);
     const uint64_t hh = lds_hash<KW>(k);
     if (p.combine) wave_combine<KW, nax(NA)>(a, p.combine, ok, k, hh, v, gidx);   // IGX_GBP_COMBINE
     if (!ok || (p.dbg & 32u)) return;
@@ -855,8 +909,9 @@ __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const 
     }
 }
 
-template <int KW, int NV, int NA>
+template <class L, int NV, int NA>
 __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
+    constexpr int KW = L::KW;
     constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
     extern __shared__ uint64_t lds[];
     AggTab<KW> T;
@@ -910,7 +965,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             if (r0 + RC < e) prefetch(r0 + RC);
             for (uint32_t u = 0; u < uc; ++u) {
                 const uint32_t i = u * PTC + threadIdx.x;
-                c_row<KW, NA>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
+                c_row<L, NA>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
             }
         }
         __syncthreads();
