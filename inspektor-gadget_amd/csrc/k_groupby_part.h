@@ -125,28 +125,6 @@ __device__ __forceinline__ bool prow_ok(const GbArgs &a, uint64_t row, const PRo
     return !a.valid || ((R.vraw >> ((uint32_t)(row & 3u) * 8u)) & 0xFFu) != 0;
 }
 
-// A record lives in LDS as rq x 4 words while it is built or read: its fields sit at
-// runtime word offsets (host-chosen layout), so LDS addressing does the packing and no
-// register array is indexed by a runtime value.
-template <class L, int NV>
-__device__ __forceinline__ void prow_stage(const PartArgs &p, uint64_t row, const PRow<L, NV> &R, uint32_t *rec) {
-    constexpr int KW = L::KW;
-    for (uint32_t q = 0; q < p.rq; ++q) reinterpret_cast<uint4 *>(rec)[q] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < KW; ++j)
-        if (p.kmsk[j]) atomicOr(rec + p.kpw[j], (R.k[j] & p.kmsk[j]) << p.ksh[j]);
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        if ((uint32_t)j < p.nv) {
-            const uint64_t raw = assemble(R.lo[j], R.hi[j], row * p.vcw[j], p.vcw[j]);
-            rec[p.rpos[j]] = (uint32_t)raw;
-            if (p.rw2[j]) rec[p.rpos[j] + 1] = (uint32_t)(raw >> 32);
-        }
-    }
-    rec[p.ipos] = (uint32_t)R.fi;
-    if (p.iw == 2) rec[p.ipos + 1] = (uint32_t)(R.fi >> 32);
-}
-
 // The record's packed key words (launch_part's rule: 1- and 2-byte columns share words, the
 // others keep theirs), known at compile time for the static key layouts: the passes then
 // decode a record with constant offsets and masks (a record's words come from one or two
@@ -191,6 +169,42 @@ struct PackKey<L, true> {
     static constexpr bool known = true;
     static constexpr PackTab T = pack_static<L>();
 };
+
+// A record lives in LDS as rq x 4 words while it is built or read: its fields sit at
+// runtime word offsets (host-chosen layout), so LDS addressing does the packing and no
+// register array is indexed by a runtime value.
+template <class L, int NV>
+__device__ __forceinline__ void prow_stage(const PartArgs &p, uint64_t row, const PRow<L, NV> &R, uint32_t *rec) {
+    constexpr int KW = L::KW;
+    if constexpr (PackKey<L>::known) {
+        // static key: packed words built in registers, the record's quads written whole
+        constexpr PackTab T = PackKey<L>::T;
+        constexpr uint32_t NW = (T.kpn + 3) / 4 * 4;
+        uint32_t w[NW] = {};
+#pragma unroll
+        for (int j = 0; j < KW; ++j)
+            if (T.kmsk[j]) w[T.kpw[j]] |= (R.k[j] & T.kmsk[j]) << T.ksh[j];
+#pragma unroll
+        for (uint32_t q = 0; q < NW / 4; ++q)
+            reinterpret_cast<uint4 *>(rec)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        for (uint32_t q = NW / 4; q < p.rq; ++q) reinterpret_cast<uint4 *>(rec)[q] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (uint32_t q = 0; q < p.rq; ++q) reinterpret_cast<uint4 *>(rec)[q] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < KW; ++j)
+            if (p.kmsk[j]) atomicOr(rec + p.kpw[j], (R.k[j] & p.kmsk[j]) << p.ksh[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        if ((uint32_t)j < p.nv) {
+            const uint64_t raw = assemble(R.lo[j], R.hi[j], row * p.vcw[j], p.vcw[j]);
+            rec[p.rpos[j]] = (uint32_t)raw;
+            if (p.rw2[j]) rec[p.rpos[j] + 1] = (uint32_t)(raw >> 32);
+        }
+    }
+    rec[p.ipos] = (uint32_t)R.fi;
+    if (p.iw == 2) rec[p.ipos + 1] = (uint32_t)(R.fi >> 32);
+}
 
 // the table's key words back from a record in LDS
 template <class L>
@@ -732,18 +746,22 @@ __device__ __forceinline__ int at_find_insert(const AggTab<KW> &T, const uint32_
         const uint4 t0 = *reinterpret_cast<const uint4 *>(T.tag + base);
         const uint4 t1 = *reinterpret_cast<const uint4 *>(T.tag + base + 4);
         const uint32_t tg[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-        uint32_t mt = 0, mb = 0, me = 0;
+        uint32_t mt = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            mt |= (tg[j] == t ? 1u : 0u) << j;
-            mb |= (tg[j] == TAG_BUSY ? 1u : 0u) << j;
-            me |= (tg[j] == 0 ? 1u : 0u) << j;
-        }
+        for (int j = 0; j < 8; ++j) mt |= (tg[j] == t ? 1u : 0u) << j;
         if (mt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         while (mt) {   // usually one candidate
             const uint32_t e = base + (uint32_t)(__builtin_ffs((int)mt) - 1);
             mt &= mt - 1;
             if (at_key_eq<KW>(T, e, k)) return (int)e;
+        }
+        // not found (a key's first record, or a tag collision): the busy and empty entries --
+        // the masks most records (repeats of a key already in the table) never need
+        uint32_t mb = 0, me = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            mb |= (tg[j] == TAG_BUSY ? 1u : 0u) << j;
+            me |= (tg[j] == 0 ? 1u : 0u) << j;
         }
         if (mb) {   // a claim in progress in this set: it may be this key
             if (++looks > SPIN_LIMIT) return -1;   // never expected; the HBM path stays exact
