@@ -212,6 +212,15 @@ int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, const char *con
 int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                   const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm);
 
+/* igx_sort_perm over a selection vector: row i of the slice is row rowmap[i] (device u32) of
+ * the key columns -- FilterEntries' result is a slice of pointers into the caller's entries
+ * (filter.go:294-325), and SortEntries sorts that slice (sort.go:116-123) without moving the
+ * entries.  pos (nullable: slice index) and valid (nullable) are read at rowmap[i].  out_perm
+ * receives the rowmap values (base rows) in sorted order: the sorted slice.  rowmap NULL ==
+ * igx_sort_perm. */
+int igx_sort_perm_ex(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
+                     const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap, uint32_t *out_perm);
+
 /* First k rows of the igx_sort_perm order (SortStats + truncate to max-rows).
  * out_idx (device u32, k).  Asynchronous. */
 int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,

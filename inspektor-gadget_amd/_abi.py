@@ -126,6 +126,7 @@ SIGNATURES = [
     ("igx_sort_prepare", _I, [C.POINTER(SchemaCol), _U32, C.POINTER(C.c_char_p), _U32,
                               C.POINTER(SortKey), C.POINTER(_U32), C.POINTER(_U32)]),
     ("igx_sort_perm", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP]),
+    ("igx_sort_perm_ex", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP, _VP]),
     ("igx_topk", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _U32, _VP]),
     ("igx_groupby_create", _I, [_VP, C.POINTER(_U32), _U32, C.POINTER(Agg), _U32, _U64,
                                 C.POINTER(_VP)]),

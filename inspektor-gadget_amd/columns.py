@@ -141,23 +141,77 @@ class Columns:
 
 class EventBatch:
     """SoA batch on the device: name -> tensor ((n,) scalars or (n, W) uint8 strings),
-    plus an optional `valid` uint8 mask (0 = nil entry, as a nil *T in the reference)."""
+    plus an optional `valid` uint8 mask (0 = nil entry, as a nil *T in the reference).
 
-    def __init__(self, cols: Columns, data: dict, valid=None):
+    A batch may be a *view*: a selection vector `sel` (u32 device tensor of row ids into the
+    base columns) over another batch's columns -- what the reference's FilterEntries and
+    SortEntries return: a fresh slice of pointers to the same entries (filter.go:294-325,
+    sort.go:116-123), no entry copied.  Taking rows of a view composes the selection; a
+    column of a view is gathered on first access (`batch[name]`, `data`, `valid`)."""
+
+    def __init__(self, cols: Columns, data: dict, valid=None, sel=None):
         self.cols = cols
-        self.data = {k.lower(): v for k, v in data.items()}
-        self.valid = valid
-        any_t = next(iter(self.data.values())) if self.data else valid
-        self.n = 0 if any_t is None else int(any_t.shape[0])
+        self._base = {k.lower(): v for k, v in data.items()}
+        self._base_valid = valid
+        any_t = next(iter(self._base.values())) if self._base else valid
+        self.base_n = 0 if any_t is None else int(any_t.shape[0])
+        self.sel = sel
+        self._mat = {}
+        self._valid_mat = None
+        self.n = self.base_n if sel is None else int(sel.shape[0])
 
     def __len__(self):
         return self.n
 
+    def _gather(self, t):
+        from . import engine                 # igx_take on the device
+        return engine.take([t], self.sel, self.base_n)[0]
+
     def __getitem__(self, name):
-        return self.data[name.lower()]
+        name = name.lower()
+        if self.sel is None:
+            return self._base[name]
+        if name not in self._mat:
+            self._mat[name] = self._gather(self._base[name])
+        return self._mat[name]
+
+    def _own(self):
+        """Turn a view into a plain batch of its rows (every column gathered once)."""
+        if self.sel is None:
+            return
+        cols = {k: self[k] for k in self._base}
+        valid = self.valid
+        self._base, self._base_valid, self.sel = cols, valid, None
+        self._mat, self._valid_mat = {}, None
+        self.base_n = self.n
+
+    @property
+    def data(self):
+        """Every column (a view becomes a plain batch of its rows first: the dict may be
+        written to)."""
+        self._own()
+        return self._base
+
+    @property
+    def valid(self):
+        if self.sel is None or self._base_valid is None:
+            return self._base_valid
+        if self._valid_mat is None:
+            self._valid_mat = self._gather(self._base_valid)
+        return self._valid_mat
+
+    @valid.setter
+    def valid(self, v):
+        self._own()
+        self._base_valid = v
+
+    def base(self):
+        """(base columns, base valid mask, selection or None) -- for passes that read a view
+        through its selection vector instead of gathering it."""
+        return self._base, self._base_valid, self.sel
 
     def device(self):
-        t = next(iter(self.data.values()))
+        t = next(iter(self._base.values()))
         return t.device
 
     def tensors_in_schema_order(self):
@@ -172,14 +226,19 @@ class EventBatch:
         return out
 
     def take(self, idx):
-        """Gather rows (device), keeping column dtypes."""
-        from . import engine                 # igx_take on the device
-        names = list(self.data.keys())
-        ts = [self.data[k] for k in names] + ([] if self.valid is None else [self.valid])
-        outs = engine.take(ts, idx, self.n)
-        out = dict(zip(names, outs[:len(names)]))
-        valid = None if self.valid is None else outs[-1]
-        return EventBatch(self.cols, out, valid)
+        """Rows idx (device ids into this batch) as a view: the selection vector composed,
+        no column copied (gather a column with batch[name], or all with materialize())."""
+        if self.sel is None:
+            sel = idx
+        else:
+            from . import engine
+            sel = engine.take([self.sel], idx, self.n)[0]
+        return EventBatch(self.cols, self._base, self._base_valid, sel=sel)
+
+    def materialize(self):
+        """This batch as a plain batch of its rows (every column gathered)."""
+        self._own()
+        return self
 
     def to_host(self):
         return {k: host(v) for k, v in self.data.items()}

@@ -653,6 +653,11 @@ extern "C" int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nke
     return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, valid, out_perm, 0, nullptr);
 }
 
+extern "C" int igx_sort_perm_ex(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
+                                const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap, uint32_t *out_perm) {
+    return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, valid, out_perm, 0, rowmap);
+}
+
 extern "C" int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                         const uint64_t *pos, uint32_t k, uint32_t *out_idx) {
     if (k == 0) return IGX_OK;

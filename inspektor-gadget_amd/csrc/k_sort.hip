@@ -28,6 +28,11 @@ namespace {
 constexpr int TB = 256;
 constexpr int IPT = 16;
 constexpr int TILE = TB * IPT;   // 4096 rows per tile
+// The radix passes' histogram and scatter kernels run a tile with 1024 threads (4 rows each):
+// at ~1M rows a pass has about one tile per CU, and a 256-thread block working through 16
+// rows per thread one barrier step at a time left the pass latency-bound (~30 us).
+constexpr int STB = 1024;
+constexpr int SIPT = TILE / STB;
 constexpr int MAXW = 80;          // composed words (keys + pos + nil; wider keys: ENOTSUP)
 constexpr int NSK = 32;           // sort keys
 
@@ -238,21 +243,34 @@ __global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict
     if (threadIdx.x == 0) sel_state_init(r, KW, n, k, st, d_n);
 }
 
-__global__ __launch_bounds__(TB) void k_radix_hist(const uint32_t *__restrict__ dw, uint32_t shift,
-                                                   uint64_t n, uint32_t nblocks,
-                                                   uint32_t *__restrict__ hist, uint32_t tile_major) {
-    __shared__ uint32_t h[256];
-    h[threadIdx.x] = 0;
+__global__ __launch_bounds__(STB) void k_radix_hist(const uint32_t *__restrict__ dw, uint32_t shift,
+                                                    uint64_t n, uint32_t nblocks,
+                                                    uint32_t *__restrict__ hist, uint32_t tile_major) {
+    // one histogram per wave (a skewed digit's same-bin adds spread over 16 copies), summed
+    __shared__ uint32_t h[STB / 64][256];
+    const uint32_t t = threadIdx.x, wave = t >> 6;
+    for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
-#pragma unroll 4
-    for (int j = 0; j < IPT; ++j) {
-        uint64_t i = base + (uint64_t)j * TB + threadIdx.x;
-        if (i < n) atomicAdd(&h[(dw[i] >> shift) & 255u], 1u);
+    uint32_t d[SIPT];
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * STB + t;
+        d[j] = i < n ? dw[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * STB + t;
+        if (i < n) atomicAdd(&h[wave][(d[j] >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (tile_major) hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
-    else hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (t < 256) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < STB / 64; ++w) c += h[w][t];
+        if (tile_major) hist[(uint64_t)blockIdx.x * 256 + t] = c;
+        else hist[(uint64_t)t * nblocks + blockIdx.x] = c;
+    }
 }
 
 // Three-phase exclusive scan over m u32 values (the [digit][tile] histogram): per-chunk
@@ -358,9 +376,12 @@ constexpr uint32_t SCAN_FREE_TILES = 512;
 // wave reads 64 digits of one tile in one request): thread t sums digit t's counts over the
 // tiles before this one and over all tiles, then the digit totals are scanned across the
 // workgroup -- the three scan kernels a pass would otherwise need
+// (called by the whole block; threads 0..255 -- digit t -- get their base, the others 0)
 __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t *tmp) {
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t t = threadIdx.x & 255u, lane = t & 63, wave = t >> 6;
+    const bool mine = threadIdx.x < 256;
     uint32_t pre = 0, tot = 0;
+    if (mine) {
     const uint32_t me = blockIdx.x;
     uint32_t q = 0;
     for (; q + 8 <= nb; q += 8) {
@@ -378,31 +399,34 @@ __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__
         tot += v;
         if (q < me) pre += v;
     }
+    }
     uint32_t inc = tot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d);
         if ((int)lane >= d) inc += y;
     }
-    if (lane == 63) tmp[wave] = inc;
+    if (mine && lane == 63) tmp[wave] = inc;
     __syncthreads();
     uint32_t ex = inc - tot;
     for (uint32_t w = 0; w < wave; ++w) ex += tmp[w];
-    return ex + pre;
+    return mine ? ex + pre : 0u;
 }
 
-__global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
+__global__ __launch_bounds__(STB) void k_radix_scatter(ScatterArgs a) {
     __shared__ uint32_t base[256], running[256];
-    __shared__ uint32_t wcnt[TB / 64][256], wpre[TB / 64][256];
+    __shared__ uint32_t wcnt[STB / 64][256], wpre[STB / 64][256];
     const uint32_t t = threadIdx.x, wave = t >> 6;
-    base[t] = a.off[(uint64_t)t * a.nblocks + blockIdx.x];
-    running[t] = 0;
-    for (int w = 0; w < TB / 64; ++w) wcnt[w][t] = 0;
+    if (t < 256) {
+        base[t] = a.off[(uint64_t)t * a.nblocks + blockIdx.x];
+        running[t] = 0;
+    }
+    for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
     const uint32_t *dw = a.in[a.dword];
-    for (int j = 0; j < IPT; ++j) {
-        const uint64_t i = tbase + (uint64_t)j * TB + t;
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = tbase + (uint64_t)j * STB + t;
         const bool valid = i < a.n;
         const uint32_t d = valid ? (dw[i] >> a.shift) & 255u : 0u;
         uint64_t peers = __ballot(valid);
@@ -415,10 +439,10 @@ __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
         const uint32_t rank = __popcll(peers & lanemask_lt());
         if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
         __syncthreads();
-        {
+        if (t < 256) {
             uint32_t r = running[t];
 #pragma unroll
-            for (int w = 0; w < TB / 64; ++w) {
+            for (int w = 0; w < STB / 64; ++w) {
                 wpre[w][t] = r;
                 r += wcnt[w][t];
                 wcnt[w][t] = 0;
@@ -434,38 +458,42 @@ __global__ __launch_bounds__(TB) void k_radix_scatter(ScatterArgs a) {
     }
 }
 
-// The same pass for at most NLMAX live words: a row's words and payload are loaded one tile
-// row ahead, so their round trip overlaps the ballots and barriers of the row before (the
+// The same pass for at most NLMAX live words: every row of the tile (SIPT per thread) is
+// loaded up front, so their round trips overlap each other and the ballots and barriers (the
 // generic kernel loads them only at the write, after both barriers).
 template <int NLMAX>
-__global__ __launch_bounds__(TB) void k_radix_scatter_pf(ScatterArgs a) {
-    __shared__ uint32_t base[256], running[256], stmp[TB / 64];
-    __shared__ uint32_t wcnt[TB / 64][256], wpre[TB / 64][256];
+__global__ __launch_bounds__(STB) void k_radix_scatter_pf(ScatterArgs a) {
+    __shared__ uint32_t base[256], running[256], stmp[4];
+    __shared__ uint32_t wcnt[STB / 64][256], wpre[STB / 64][256];
     const uint32_t t = threadIdx.x, wave = t >> 6;
-    base[t] = a.off ? a.off[(uint64_t)t * a.nblocks + blockIdx.x] : tile_digit_base(a.cnt, a.nblocks, stmp);
-    running[t] = 0;
-    for (int w = 0; w < TB / 64; ++w) wcnt[w][t] = 0;
+    const uint32_t b0 = a.off ? (t < 256 ? a.off[(uint64_t)t * a.nblocks + blockIdx.x] : 0u)
+                              : tile_digit_base(a.cnt, a.nblocks, stmp);
+    if (t < 256) {
+        base[t] = b0;
+        running[t] = 0;
+    }
+    for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
-    uint32_t cw[NLMAX], nw[NLMAX], cp = 0, np = 0;
-    auto load = [&](int j, uint32_t (&wv)[NLMAX], uint32_t &pv) {
-        const uint64_t i = tbase + (uint64_t)j * TB + t;
+    uint32_t cw[SIPT][NLMAX], cp[SIPT];
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = tbase + (uint64_t)j * STB + t;
         if (i < a.n) {
 #pragma unroll
             for (int w = 0; w < NLMAX; ++w)
-                if ((uint32_t)w < a.nlive) wv[w] = a.in[w][i];
-            pv = a.pin[i];
+                if ((uint32_t)w < a.nlive) cw[j][w] = a.in[w][i];
+            cp[j] = a.pin[i];
         }
-    };
-    load(0, cw, cp);
-    for (int j = 0; j < IPT; ++j) {
-        if (j + 1 < IPT) load(j + 1, nw, np);
-        const uint64_t i = tbase + (uint64_t)j * TB + t;
+    }
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = tbase + (uint64_t)j * STB + t;
         const bool valid = i < a.n;
         uint32_t dv = 0;
 #pragma unroll
         for (int w = 0; w < NLMAX; ++w)
-            if ((uint32_t)w == a.dword) dv = cw[w];
+            if ((uint32_t)w == a.dword) dv = cw[j][w];
         const uint32_t d = valid ? (dv >> a.shift) & 255u : 0u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -477,10 +505,10 @@ __global__ __launch_bounds__(TB) void k_radix_scatter_pf(ScatterArgs a) {
         const uint32_t rank = __popcll(peers & lanemask_lt());
         if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
         __syncthreads();
-        {
+        if (t < 256) {
             uint32_t r = running[t];
 #pragma unroll
-            for (int w = 0; w < TB / 64; ++w) {
+            for (int w = 0; w < STB / 64; ++w) {
                 wpre[w][t] = r;
                 r += wcnt[w][t];
                 wcnt[w][t] = 0;
@@ -492,12 +520,9 @@ __global__ __launch_bounds__(TB) void k_radix_scatter_pf(ScatterArgs a) {
             const uint64_t pos = (uint64_t)base[d] + wpre[wave][d] + rank;
 #pragma unroll
             for (int w = 0; w < NLMAX; ++w)
-                if ((uint32_t)w < a.nlive) a.out[w][pos] = cw[w];
-            a.pout[pos] = cp;
+                if ((uint32_t)w < a.nlive) a.out[w][pos] = cw[j][w];
+            a.pout[pos] = cp[j];
         }
-#pragma unroll
-        for (int w = 0; w < NLMAX; ++w) cw[w] = nw[w];
-        cp = np;
     }
 }
 
@@ -1273,17 +1298,17 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             sa.pin = P[cur];
             sa.pout = P[cur ^ 1];
             const bool scan_free = nl <= 8 && nblocks <= SCAN_FREE_TILES;
-            hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(TB), 0, ctx->stream,
+            hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(STB), 0, ctx->stream,
                                sa.in[dslot], sa.shift, nrows, nblocks, hist, scan_free ? 1u : 0u);
             sa.off = scan_free ? nullptr : hist;
             sa.cnt = hist;
             if (!scan_free) launch_scan(ctx->stream, hist, (uint64_t)256 * nblocks, scan_part);
             if (nl <= 4)
-                hipLaunchKernelGGL(k_radix_scatter_pf<4>, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter_pf<4>, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
             else if (nl <= 8)
-                hipLaunchKernelGGL(k_radix_scatter_pf<8>, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter_pf<8>, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
             else
-                hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(TB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
             // swap buffers: the next pass reads what this one wrote
             cur ^= 1;
             for (uint32_t l = 0; l < nl; ++l) {

@@ -165,8 +165,10 @@ def take(tensors, idx, nrows=None, pad=False):
 # ------------------------------------------------------------------------------------
 # sort
 # ------------------------------------------------------------------------------------
-def sort_perm(keys, n, pos=None, valid=None, k=None):
-    """keys: list of (tensor, desc) in sortBy order.  Returns u32 permutation (first k)."""
+def sort_perm(keys, n, pos=None, valid=None, k=None, rowmap=None):
+    """keys: list of (tensor, desc) in sortBy order.  Returns u32 permutation (first k).
+    rowmap (u32, n rows): sort the selection vector -- row i is row rowmap[i] of the key
+    columns, valid and pos (igx_sort_perm_ex); the result is then rowmap values in order."""
     torch = torch_mod()
     ctx = context()
     dev = keys[0][0].device if keys else (pos.device if pos is not None else "cuda")
@@ -181,7 +183,11 @@ def sort_perm(keys, n, pos=None, valid=None, k=None):
     out = torch.empty(max(1, m), dtype=torch.uint32, device=dev)
     if n == 0:
         return out[:0]
-    if k is None:
+    if rowmap is not None:
+        if k is not None:
+            raise ValueError("a top-K over a selection vector: sort the view first")
+        ctx.check(ctx.L.igx_sort_perm_ex(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(rowmap), ptr(out)))
+    elif k is None:
         ctx.check(ctx.L.igx_sort_perm(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(out)))
     else:
         if valid is not None:

@@ -58,10 +58,20 @@ class ColumnSorterCollection:
         return engine.sort_perm_kinds(keys, batch.n, pos=pos, valid=batch.valid, k=k)
 
     def Sort(self, batch: EventBatch, pos=None):
-        """Returns the batch in sorted order (the reference sorts []*T in place)."""
+        """Returns the batch in sorted order (the reference sorts []*T in place).  A view (a
+        filtered slice of pointers) is sorted through its selection vector: the result is the
+        same entries' row ids in sorted order, no column read beyond the sort keys."""
         if batch is None or batch.n == 0:
             return batch
-        return batch.take(self.Perm(batch, pos))
+        base, base_valid, sel = batch.base()
+        if sel is None or pos is not None:
+            return batch.take(self.Perm(batch, pos))
+        ordered = self.cols.GetOrderedColumns()
+        keys = [(base[ordered[sk.col].Name.lower()], bool(sk.desc), sk.kind) for sk in self.keys]
+        if sel.dtype != torch_mod().int32 and sel.dtype != torch_mod().uint32:
+            sel = sel.to(torch_mod().int32)
+        out = engine.sort_perm_kinds(keys, batch.n, valid=base_valid, rowmap=sel.contiguous())
+        return EventBatch(batch.cols, base, base_valid, sel=out)
 
 
 def Prepare(cols: Columns, sort_by) -> ColumnSorterCollection:
