@@ -373,34 +373,42 @@ struct ScatterArgs {
 constexpr uint32_t SCAN_FREE_TILES = 512;
 
 // this tile's base of every digit from the raw counts, stored tile-major ([tile][digit]: a
-// wave reads 64 digits of one tile in one request): thread t sums digit t's counts over the
-// tiles before this one and over all tiles, then the digit totals are scanned across the
-// workgroup -- the three scan kernels a pass would otherwise need
-// (called by the whole block; threads 0..255 -- digit t -- get their base, the others 0)
+// wave reads 64 digits of one tile in one request): the block's four 256-thread quarters each
+// sum digit t's counts over a quarter of the tiles (before this one, and all), 16 loads in
+// flight per thread; the quarters' sums meet in LDS and the digit totals are scanned across
+// the first 256 threads -- the three scan kernels a pass would otherwise need.  Called by the
+// whole block; threads 0..255 get digit t's base, the others 0.  tmp: 4 + 2 x 1024 words.
 __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t *tmp) {
-    const uint32_t t = threadIdx.x & 255u, lane = t & 63, wave = t >> 6;
-    const bool mine = threadIdx.x < 256;
-    uint32_t pre = 0, tot = 0;
-    if (mine) {
+    const uint32_t t = threadIdx.x & 255u, part = threadIdx.x >> 8, lane = t & 63, wave = t >> 6;
     const uint32_t me = blockIdx.x;
-    uint32_t q = 0;
-    for (; q + 8 <= nb; q += 8) {
-        uint32_t v[8];
+    const uint32_t q0 = (uint32_t)((uint64_t)nb * part / 4), q1 = (uint32_t)((uint64_t)nb * (part + 1) / 4);
+    uint32_t pre = 0, tot = 0;
+    uint32_t q = q0;
+    for (; q + 16 <= q1; q += 16) {
+        uint32_t v[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = cnt[(uint64_t)(q + u) * 256 + t];
+        for (int u = 0; u < 16; ++u) v[u] = cnt[(uint64_t)(q + u) * 256 + t];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 16; ++u) {
             tot += v[u];
             if (q + u < me) pre += v[u];
         }
     }
-    for (; q < nb; ++q) {
+    for (; q < q1; ++q) {
         const uint32_t v = cnt[(uint64_t)q * 256 + t];
         tot += v;
         if (q < me) pre += v;
     }
+    uint32_t *spre = tmp + 4, *stot = tmp + 4 + 1024;
+    spre[threadIdx.x] = pre;
+    stot[threadIdx.x] = tot;
+    __syncthreads();
+    const bool mine = threadIdx.x < 256;
+    if (mine) {
+        pre = spre[t] + spre[256 + t] + spre[512 + t] + spre[768 + t];
+        tot = stot[t] + stot[256 + t] + stot[512 + t] + stot[768 + t];
     }
-    uint32_t inc = tot;
+    uint32_t inc = mine ? tot : 0u;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d);
@@ -408,7 +416,7 @@ __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__
     }
     if (mine && lane == 63) tmp[wave] = inc;
     __syncthreads();
-    uint32_t ex = inc - tot;
+    uint32_t ex = inc - (mine ? tot : 0u);
     for (uint32_t w = 0; w < wave; ++w) ex += tmp[w];
     return mine ? ex + pre : 0u;
 }
@@ -463,7 +471,7 @@ __global__ __launch_bounds__(STB) void k_radix_scatter(ScatterArgs a) {
 // generic kernel loads them only at the write, after both barriers).
 template <int NLMAX>
 __global__ __launch_bounds__(STB) void k_radix_scatter_pf(ScatterArgs a) {
-    __shared__ uint32_t base[256], running[256], stmp[4];
+    __shared__ uint32_t base[256], running[256], stmp[4 + 2 * STB];
     __shared__ uint32_t wcnt[STB / 64][256], wpre[STB / 64][256];
     const uint32_t t = threadIdx.x, wave = t >> 6;
     const uint32_t b0 = a.off ? (t < 256 ? a.off[(uint64_t)t * a.nblocks + blockIdx.x] : 0u)
