@@ -336,3 +336,17 @@ def test_many_sort_keys(oracle, E, H, torch):
     ref = oracle.go_sort_entries(keys_o, n)
     assert np.array_equal(H.host(E.sort_perm(keys_d, n)), ref)
     assert np.array_equal(H.host(E.sort_perm(keys_d, n, k=50)), ref[:50])
+
+
+def test_nan_sort_hand_derived_vectors(igx, torch):
+    """The device NaN path (k_gostable.hip) on the hand-derived Go SliceStable orders of
+    tests/test_oracle_golden.py NAN_VECTORS (float64 and float32 keys, nil rows)."""
+    from test_oracle_golden import NAN_VECTORS
+    E, H = igx.engine, igx.columns
+    for keys, valid, want in NAN_VECTORS:
+        n = len(want)
+        dv = None if valid is None else H.to_device(np.array(valid, np.uint8))
+        for dt in (np.float64, np.float32):
+            cols = [(H.to_device(np.array(v, dt)), d) for v, d in keys]
+            got = H.host(E.sort_perm(cols, n, valid=dv)).astype(np.int64)
+            assert list(got) == want, (keys, valid, dt)

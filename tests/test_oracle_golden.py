@@ -262,3 +262,40 @@ def test_go_stable_with_nan_c_matches_py(oracle, trial):
         # nil rows come back as None from the py version, in order of their row ids
         nil_rows = iter([r for r in cperm if not valid[r]])
         assert [r if r is not None else next(nil_rows) for r in py] == list(cperm)
+
+
+# Hand-derived Go 1.19 SliceStable orders with NaN keys (the NaN path was pinned
+# only C-vs-Python).  n < 20, so SliceStable is one insertionSort pass per key
+# (sort/zsortfunc.go insertionSort_func); less = !(a < b) != asc (sort.go:125-135), i.e.
+# a < b for ASC and !(a < b) for DESC, which is true whenever a NaN is involved.  Each
+# expectation below was stepped through by hand; nil rows sort last (less(nil, x) = false,
+# less(x, nil) = true).  Entries: (keys in sortBy order as (values, desc), valid, expected).
+NAN = float("nan")
+NAN_VECTORS = [
+    ([([3.0, NAN, 1.0, 2.0], False)], None, [0, 1, 2, 3]),     # no adjacent pair is `<`-ordered
+    ([([NAN, 2.0, 1.0], False)], None, [0, 2, 1]),
+    ([([2.0, 1.0, NAN, 0.0], False)], None, [1, 0, 2, 3]),      # the NaN walls 0.0 off
+    ([([1.0, NAN, 2.0], True)], None, [2, 1, 0]),
+    ([([NAN, NAN, 5.0], True)], None, [2, 1, 0]),
+    ([([0.0, NAN, 0.0, 1.0], True)], None, [3, 2, 1, 0]),       # DESC swaps every tie and NaN
+    ([([NAN, 7.0, 1.0], False)], [1, 0, 1], [0, 2, 1]),         # nil row 1 sinks, NaN stays first
+    # two keys: the last key's pass runs first ([2, 1, 0]), then k0's pass meets [1, NaN, 0]
+    # and moves nothing: row 0 (k0 = 0) stays behind row 2 (k0 = 1)
+    ([([0.0, NAN, 1.0], False), ([2.0, 1.0, 0.0], False)], None, [2, 1, 0]),
+]
+
+
+@pytest.mark.parametrize("case", range(len(NAN_VECTORS)))
+def test_go_stable_nan_hand_derived(oracle, case):
+    O = oracle
+    keys, valid, want = NAN_VECTORS[case]
+    n = len(want)
+    v8 = None if valid is None else np.array(valid, np.uint8)
+    got = O.go_sort_entries([(np.array(v, np.float64), "float64", d) for v, d in keys], n, valid=v8)
+    assert list(got) == want
+    got32 = O.go_sort_entries([(np.array(v, np.float32), "float32", d) for v, d in keys], n, valid=v8)
+    assert list(got32) == want
+    rows = [r if valid is None or valid[r] else None for r in range(n)]
+    py = O.go_sort_entries_py(rows, [(lambda r, v=v: v[r], d) for v, d in keys])
+    nil_rows = iter([r for r in want if valid is not None and not valid[r]])
+    assert [r if r is not None else next(nil_rows) for r in py] == want

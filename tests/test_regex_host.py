@@ -250,3 +250,20 @@ def test_filter_table_regex_rows_on_the_automaton(igx):
         assert rc == 0
         cnt = sum(run_blob(blob, s.encode()) != neg for s in strings)
         assert cnt == row["count"], f
+
+
+def test_regex_script_table_boundaries(igx):
+    r"""Fixed boundary runes of the generated script tables (tools/gen_unicode.py, Unicode
+    13.0.0 = Go 1.19's unicode.Version; Python 3.10's unicodedata is also 13.0.0, which names
+    the assigned runes used here).  Han ends at U+9FFC in 13.0 (U+9FFD is 14.0); Inherited
+    runs U+0300-U+036F and U+0370 is Greek; '@' is Common and 'A' Latin; U+1F978 (13.0) is
+    Common while U+1FAE0 (14.0) is unassigned, so neither Common nor any other script."""
+    ok = lambda p, r: run_blob(compile_blob(igx, p.encode())[1], chr(r).encode())   # noqa: E731
+    assert ok(r"^\p{Han}$", 0x9FFC) and not ok(r"^\p{Han}$", 0x9FFD) and ok(r"^\p{Han}$", 0x4E00)
+    assert ok(r"^\p{Han}$", 0x3400) and not ok(r"^\p{Han}$", 0x33FF)
+    assert ok(r"^\p{Inherited}$", 0x0300) and ok(r"^\p{Inherited}$", 0x036F)
+    assert not ok(r"^\p{Inherited}$", 0x0370) and ok(r"^\p{Greek}$", 0x0370)
+    assert not ok(r"^\p{Inherited}$", 0x02FF) and ok(r"^\p{Common}$", 0x02FF)
+    assert ok(r"^\p{Common}$", 0x40) and not ok(r"^\p{Common}$", 0x41) and ok(r"^\p{Latin}$", 0x41)
+    assert ok(r"^\p{Common}$", 0x1F978) and not ok(r"^\p{Common}$", 0x1FAE0)
+    assert ok(r"^\P{Common}$", 0x1FAE0) and not ok(r"^\p{Han}$", 0x1FAE0)
