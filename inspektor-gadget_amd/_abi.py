@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libigx.so")
+LIB_PATH = os.environ.get("IGX_LIB") or os.path.join(HERE, "libigx.so")   # IGX_LIB: A/B builds
 
 IGX_OK = 0
 IGX_ENOENT = -2

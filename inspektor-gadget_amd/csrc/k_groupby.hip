@@ -2017,34 +2017,41 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     // B tiles: as many records (a multiple of PTA, at most 4096) as the tile LDS holds
     uint32_t trb = 4096;
     while (trb > PTA && (size_t)trb * (16 * p.rq + 6) + 12 * PART_F_MAX + 72 > PART_TILE_LDS) trb -= PTA;
+    if (const char *d = std::getenv("IGX_GBP_TRB"))   // tuning knob: records per B tile (a multiple of PTA)
+        trb = std::max<uint32_t>(PTA, std::min<uint32_t>(trb, (uint32_t)std::strtoul(d, nullptr, 0) / PTA * PTA));
     p.trb = trb;
     p.ch = (uint32_t)std::max<uint64_t>(8192, 4 * (a.n / NB + 1));
     p.tiles_a = (uint32_t)((a.n + TRA - 1) / TRA);
     p.nchunk = (p.tiles_a + CHT - 1) / CHT;
-    const uint64_t tiles_b = a.n / trb + F1 + 1;
+    const uint32_t S1 = region ? 1u << PART_S1_LOG : 1u, U1 = F1 * S1;   // first-level runs (slices)
+    const uint64_t tiles_b = a.n / trb + U1 + 1;
+    uint32_t c2pad = 16;   // final-region cursors one 64-B line apart (pass B's atomics)
+    if (const char *d = std::getenv("IGX_GBP_C2PAD")) c2pad = std::max<uint32_t>(1, (uint32_t)std::strtoul(d, nullptr, 0));
     const uint64_t items_max = NB + a.n / p.ch + 1;
-    uint64_t r1 = a.n * 5 / 4 / F1 + TRA, r2 = a.n * 5 / 4 / NB + 1024;   // region records
+    uint64_t r1 = a.n * 5 / 4 / U1 + TRA, r2 = a.n * 5 / 4 / NB + 1024;   // region records
     if (const char *d = std::getenv("IGX_GBP_REGSIZE"))   // tests: small regions overflow
         r1 = r2 = std::max<uint64_t>(1, std::strtoull(d, nullptr, 0));
-    if (region && (r1 * F1 >= (1ull << 31) || r2 * NB >= (1ull << 31))) region = false;
+    if (region && (r1 * U1 >= (1ull << 31) || r2 * NB >= (1ull << 31))) region = false;
     if (region) {
         p.reg1 = (uint32_t)r1;
         p.reg2 = (uint32_t)r2;
+        p.s1log = PART_S1_LOG;
+        p.c2pad = c2pad;
         // scratch: rc1 | rc2 | tstart | bt | istart | itfb | ctl (u32 words)
-        const uint64_t words = F1 + NB + (F1 + 1) + tiles_b + (NB + 1) + items_max + 4;
+        const uint64_t words = U1 * RC1_PAD + NB * c2pad + (U1 + 1) + tiles_b + (NB + 1) + items_max + 4;
         int rc = grow(ctx, reinterpret_cast<void **>(&t->p_cnt), &t->p_cnt_bytes, 4 * words);
         if (!rc) rc = grow(ctx, reinterpret_cast<void **>(&t->p_recs), &t->p_recs_bytes,
-                           (size_t)16 * p.rq * (r1 * F1 + r2 * NB));
+                           (size_t)16 * p.rq * (r1 * U1 + r2 * NB));
         if (rc) return rc;
         p.rc1 = t->p_cnt;
-        p.rc2 = p.rc1 + F1;
-        p.tstart = p.rc2 + NB;
-        p.bt = p.tstart + F1 + 1;
+        p.rc2 = p.rc1 + U1 * RC1_PAD;
+        p.tstart = p.rc2 + NB * c2pad;
+        p.bt = p.tstart + U1 + 1;
         p.istart = p.bt + tiles_b;
         p.itfb = p.istart + NB + 1;
         p.ctl = p.itfb + items_max;
         p.recs1 = t->p_recs;
-        p.recs2 = t->p_recs + r1 * F1 * p.rq * 4;
+        p.recs2 = t->p_recs + r1 * U1 * p.rq * 4;
     }
     // scratch: cnt1 | csum | hist | start2 | cur2 | tstart | bt | istart | itfb | ctl (u32 words)
     const uint64_t w_cnt1 = (uint64_t)p.tiles_a * F1, w_csum = (uint64_t)p.nchunk * F1;
@@ -2087,7 +2094,7 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     }
     const uint32_t cus = (uint32_t)ctx->num_cus;
     if (region) {
-        IGX_HIP(ctx, hipMemsetAsync(p.rc1, 0, 4ull * (F1 + NB), ctx->stream));
+        IGX_HIP(ctx, hipMemsetAsync(p.rc1, 0, 4ull * (U1 * RC1_PAD + NB * p.c2pad), ctx->stream));
         hipLaunchKernelGGL((k_gbp_a<L, NV>), dim3(p.tiles_a), dim3(PTA), lds_a, ctx->stream, a, p);
         if (p.dbg & 256u) return IGX_OK;   // diagnostics: stop after pass A (the table is left unset)
         hipLaunchKernelGGL(k_gbr_tiles, dim3(1), dim3(1024), 0, ctx->stream, p);

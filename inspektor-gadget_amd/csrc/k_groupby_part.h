@@ -41,6 +41,9 @@ constexpr uint32_t PART_LB_MAX = 15;           // final buckets <= 2^15 (count-p
 constexpr uint32_t PART_F_MAX = 256;           // buckets per scatter level (one per thread)
 constexpr uint32_t PNV = 2 * AMAX;             // distinct value / condition columns a record carries
 constexpr uint32_t CHT = 64;                   // A tiles per chunk of the offset scan
+constexpr uint32_t RC1_PAD = 16;               // words between two slice cursors of pass A
+constexpr uint32_t PART_S1_LOG = 3;            // slices per first-level region (regions)
+constexpr uint32_t PART_U1_MAX = PART_F_MAX << PART_S1_LOG;
 
 struct PartArgs {
     uint32_t *recs1, *recs2;   // records after pass A / pass B (rq quads each)
@@ -50,7 +53,8 @@ struct PartArgs {
     uint32_t *hist;            // NB: rows per final bucket (pass K)
     uint32_t *start2;          // NB + 1: first record of each final bucket (prefix of hist)
     uint32_t *cur2;            // NB: pass B's write cursors (final buckets)
-    uint32_t *tstart;          // F1 + 1: first B tile of each first-level bucket
+    uint32_t *tstart;          // F1 + 1 (regions: U1 + 1): first B tile of each first-level bucket
+                               // (regions: of each slice)
     uint32_t *bt;              // B tile -> first-level bucket
     uint32_t *istart;          // NB + 1: first C work item of each final bucket
     uint32_t *itfb;            // C work item -> final bucket
@@ -85,8 +89,14 @@ struct PartArgs {
     // region variant (no count pass): bucket b's records fill a fixed region of reg records
     // through a cursor (one atomic per (tile, bucket)); a record past its region merges into
     // the table directly (find-or-insert + atomics: exact on any stream)
-    uint32_t *rc1, *rc2;       // F1 / NB region cursors (records reserved; may pass the region)
-    uint32_t reg1, reg2;       // records per first-level / final region (0: exact runs)
+    // Pass A's cursors are the most contended words of the form (every A tile adds to each of
+    // the F1): a first-level region is cut into 2^s1log slices, A tile t fills slice
+    // t mod 2^s1log, and each slice's cursor has a 64-B line of its own (RC1_PAD words)
+    uint32_t *rc1, *rc2;       // U1 = F1 << s1log slice cursors (stride RC1_PAD) / NB final-region
+                               // cursors (records reserved; may pass the region)
+    uint32_t reg1, reg2;       // records per first-level slice / final region (0: exact runs)
+    uint32_t s1log;            // log2 slices per first-level region (0 in the exact form)
+    uint32_t c2pad;            // words between two final-region cursors (rc2)
 };
 
 // record words (compile-time bound): packed key words, loaded columns, index
@@ -94,7 +104,13 @@ template <int KW, int NV>
 constexpr int part_w() { return (KW + 2 * NV + 2 + 3) & ~3; }
 // rows per thread of passes K and A (a row's loaded dwords stay in registers)
 template <int KW, int NV>
-constexpr int part_rows() { return KW + 1 + 2 * NV <= 8 ? 8 : 4; }
+constexpr int part_rows() {
+#ifdef IGX_PART_R
+    return IGX_PART_R;
+#else
+    return KW + 1 + 2 * NV <= 8 ? 8 : 4;
+#endif
+}
 
 // a row's loads: nil mask, key columns, the loaded value / condition columns, index column
 template <class L, int NV>
@@ -507,7 +523,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     uint8_t *sb = lds_raw + (size_t)TRA * rq * 16;                       // TRA: bucket of each position
     uint32_t *hist = reinterpret_cast<uint32_t *>(sb + TRA);             // F
     uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = blockIdx.x, sl = t & ((1u << p.s1log) - 1u);   // region slice of this tile
     if (threadIdx.x < F) {
         hist[threadIdx.x] = 0;
         if (!p.reg1) base[threadIdx.x] = p.cnt1[(uint64_t)t * F + threadIdx.x];
@@ -536,7 +552,7 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     if (threadIdx.x < F) {
         off[threadIdx.x] = o;
         const uint32_t hc = hist[threadIdx.x];   // region variant: this tile's run at the bucket's cursor
-        if (p.reg1) base[threadIdx.x] = hc ? atomicAdd(p.rc1 + threadIdx.x, hc) : 0u;
+        if (p.reg1) base[threadIdx.x] = hc ? atomicAdd(p.rc1 + ((threadIdx.x << p.s1log) + sl) * RC1_PAD, hc) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -561,31 +577,35 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
         bool spill = false;
         if (!live) {
         } else if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
-        else if (g < p.reg1) out[((uint64_t)b * p.reg1 + g) * rq + q] = stage[qi];
+        else if (g < p.reg1) out[((uint64_t)((b << p.s1log) + sl) * p.reg1 + g) * rq + q] = stage[qi];
         else spill = q == 0;
         if (p.reg1) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? j : 0u) * rq));
     }
 }
 
-// region variant, between A and B: B tiles of each first-level region (tstart, bt, ctl[1])
+// region variant, between A and B: B tiles of each first-level slice (tstart, bt, ctl[1])
 __global__ __launch_bounds__(1024) void k_gbr_tiles(PartArgs p) {
     __shared__ uint32_t wsum[17];
-    __shared__ uint32_t ts[PART_F_MAX + 1];
-    const uint32_t F1 = 1u << p.f1;
-    const uint32_t c = threadIdx.x < F1 ? min(p.rc1[threadIdx.x], p.reg1) : 0u;
+    __shared__ uint32_t ts[PART_U1_MAX + 1];
+    const uint32_t U1 = 1u << (p.f1 + p.s1log);
+    const uint32_t per = (U1 + 1023) / 1024, u0 = threadIdx.x * per;
+    uint32_t nt = 0;
+    for (uint32_t i = 0; i < per; ++i)
+        if (u0 + i < U1) nt += (min(p.rc1[(u0 + i) * RC1_PAD], p.reg1) + p.trb - 1) / p.trb;
     uint32_t tot;
-    const uint32_t st = block_excl_scan((c + p.trb - 1) / p.trb, wsum, tot);
-    if (threadIdx.x < F1) {
-        p.tstart[threadIdx.x] = st;
-        ts[threadIdx.x] = st;
+    uint32_t st = block_excl_scan(nt, wsum, tot);
+    for (uint32_t i = 0; i < per && u0 + i < U1; ++i) {
+        p.tstart[u0 + i] = st;
+        ts[u0 + i] = st;
+        st += (min(p.rc1[(u0 + i) * RC1_PAD], p.reg1) + p.trb - 1) / p.trb;
     }
     if (threadIdx.x == 0) {
-        p.tstart[F1] = tot;
-        ts[F1] = tot;
+        p.tstart[U1] = tot;
+        ts[U1] = tot;
         p.ctl[1] = tot;
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tot; t += 1024) p.bt[t] = upper_bound_u32(ts, 0, F1 + 1, t) - 1;
+    for (uint32_t t = threadIdx.x; t < tot; t += 1024) p.bt[t] = upper_bound_u32(ts, 0, U1 + 1, t) - 1;
 }
 
 // region variant, after B: C work items from the final regions' fills (a final bucket larger
@@ -597,7 +617,7 @@ __global__ __launch_bounds__(1024) void k_gbr_items(PartArgs p) {
     uint32_t si = 0;
     for (uint32_t i = 0; i < per; ++i) {
         const uint32_t b = b0 + i;
-        const uint32_t c = b < NB ? min(p.rc2[b], p.reg2) : 0u;
+        const uint32_t c = b < NB ? min(p.rc2[b * p.c2pad], p.reg2) : 0u;
         si += (c + p.ch - 1) / p.ch;
     }
     uint32_t toti;
@@ -605,7 +625,7 @@ __global__ __launch_bounds__(1024) void k_gbr_items(PartArgs p) {
     for (uint32_t i = 0; i < per; ++i) {
         const uint32_t b = b0 + i;
         if (b >= NB) break;
-        const uint32_t c = min(p.rc2[b], p.reg2), ni = (c + p.ch - 1) / p.ch;
+        const uint32_t c = min(p.rc2[b * p.c2pad], p.reg2), ni = (c + p.ch - 1) / p.ch;
         p.istart[b] = runi;
         for (uint32_t k = 0; k < ni; ++k) p.itfb[runi + k] = b;
         runi += ni;
@@ -634,11 +654,11 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     uint16_t *rank = bkt + trb, *perm = rank + trb;
     uint32_t *hist = reinterpret_cast<uint32_t *>(perm + trb);
     uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
-    const uint32_t b1 = p.bt[tile];
-    const uint32_t j = tile - p.tstart[b1];
-    // exact runs: first-level bucket b1 spans final buckets' starts; regions: [b1 reg1, + fill)
-    const uint32_t s = p.reg1 ? b1 * p.reg1 + j * trb : p.start2[b1 << p.f2] + j * trb;
-    const uint32_t e = p.reg1 ? b1 * p.reg1 + min(min(p.rc1[b1], p.reg1), (j + 1) * trb)
+    const uint32_t u = p.bt[tile], b1 = u >> p.s1log;   // slice u of first-level bucket b1
+    const uint32_t j = tile - p.tstart[u];
+    // exact runs: first-level bucket b1 spans final buckets' starts; regions: [u reg1, + fill)
+    const uint32_t s = p.reg1 ? u * p.reg1 + j * trb : p.start2[b1 << p.f2] + j * trb;
+    const uint32_t e = p.reg1 ? u * p.reg1 + min(min(p.rc1[u * RC1_PAD], p.reg1), (j + 1) * trb)
                               : min(p.start2[(b1 + 1) << p.f2], s + trb);
     const uint32_t cnt = e - s;
     if (threadIdx.x < F) hist[threadIdx.x] = 0;
@@ -667,7 +687,8 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
     const uint32_t o = block_excl_scan(c, wsum, total);
     if (threadIdx.x < F) {
         off[threadIdx.x] = o;
-        base[threadIdx.x] = c ? atomicAdd((p.reg2 ? p.rc2 : p.cur2) + (b1 << p.f2) + threadIdx.x, c) : 0u;
+        const uint32_t fb = (b1 << p.f2) + threadIdx.x;
+        base[threadIdx.x] = c ? atomicAdd(p.reg2 ? p.rc2 + fb * p.c2pad : p.cur2 + fb, c) : 0u;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += PTA) perm[off[bkt[i]] + rank[i]] = (uint16_t)i;
@@ -959,7 +980,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         const uint32_t fb = p.itfb[it];
         const uint32_t i0 = p.istart[fb], nit = p.istart[fb + 1] - i0, kx = it - i0;
         const uint32_t s0 = p.reg2 ? fb * p.reg2 : p.start2[fb];
-        const uint32_t len = p.reg2 ? min(p.rc2[fb], p.reg2) : p.start2[fb + 1] - s0;
+        const uint32_t len = p.reg2 ? min(p.rc2[fb * p.c2pad], p.reg2) : p.start2[fb + 1] - s0;
         const uint32_t s = s0 + (uint32_t)((uint64_t)len * kx / nit);
         const uint32_t e = s0 + (uint32_t)((uint64_t)len * (kx + 1) / nit);
         const uint64_t qlast = (uint64_t)e * rq - 1;   // the item's last quad (loads clamp to it)
