@@ -1996,7 +1996,8 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
         const int64_t occw = (int64_t)1 << (t->sbits - lb - 5);
         const int64_t room = (int64_t)PART_AGG_LDS - (int64_t)stage_c - 8 * occw - 16;
         if (room < (int64_t)(8 * entry)) return 0u;
-        return (uint32_t)std::min<int64_t>(65528, room / (int64_t)entry) & ~7u;   // whole 8-way sets
+        // whole 8-way sets, E a multiple of 16: the byte tags keep what follows them 16-B aligned
+        return (uint32_t)std::min<int64_t>(65520, room / (int64_t)entry) & ~15u;
     };
     uint32_t lb = 0;
     while (lb < lb_max && (double)(t->cap >> lb) > 0.9 * entries(lb)) ++lb;
@@ -2006,9 +2007,9 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     p.sb_log = t->sbits - lb;
     p.occw = 1u << (p.sb_log - 5);
     p.E = entries(lb);
-    if (p.E < 8) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: key of %u words too wide for the partitioned form", KW);
+    if (p.E < 16) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: key of %u words too wide for the partitioned form", KW);
     if (const char *d = std::getenv("IGX_GBP_ENTRIES"))   // tests: a small LDS table overflows
-        p.E = std::max<uint32_t>(8, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0))) & ~7u;
+        p.E = std::max<uint32_t>(16, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0))) & ~15u;
     p.maxp = std::min<uint32_t>(p.E / 8, 32);   // sets probed before a row takes the HBM path
     p.combine = 0;   // wave pre-combine: measured slower on C4 and C5
     if (const char *d = std::getenv("IGX_GBP_COMBINE")) p.combine = (uint32_t)std::strtoul(d, nullptr, 0);

@@ -716,17 +716,17 @@ template <int KW>
 struct AggTab {
     uint64_t *first;     // E: min event index (~0 = none yet)
     uint64_t *agg;       // naggs x E
-    uint32_t *tag;       // E: 0 = empty, TAG_BUSY = claimed, key being written, else the hash's low
-                         // word | 1 (odd: published, the key words are valid)
+    uint8_t *tag;        // E: 0 = empty, TAG_BUSY = claimed, key being written, else 0x80 | 7 bits
+                         // of the LDS hash (published: the key words are valid)
     uint32_t *key;       // E x KW
     uint32_t *occ_old;   // occw: the bucket's occupancy bitmap words before this flush
     uint32_t *occ_new;   // occw: slots claimed by this flush
     uint32_t *flag;      // [0] some row of the item took the HBM path, [1] the item
     uint32_t E;
 };
-constexpr uint32_t TAG_BUSY = 2;
+constexpr uint32_t TAG_BUSY = 1;
 
-__host__ __device__ constexpr size_t agg_entry_bytes(uint32_t kw, uint32_t naggs) { return 12 + 4 * (size_t)kw + 8 * (size_t)naggs; }
+__host__ __device__ constexpr size_t agg_entry_bytes(uint32_t kw, uint32_t naggs) { return 9 + 4 * (size_t)kw + 8 * (size_t)naggs; }
 
 // every key word of entry e compared with k: all loads issued before any compare (a
 // short-circuit compare is one dependent LDS round trip per word)
@@ -750,53 +750,54 @@ __device__ __forceinline__ bool at_key_eq(const AggTab<KW> &T, uint32_t e, const
     return diff == 0;
 }
 
+// 0x80 in each byte of x that is zero, 0 elsewhere (exact: no borrow between bytes)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
 // find or insert the key's entry; -1 when maxp sets were probed without a match or a free
-// entry (the row then goes to HBM).  The table is 8-way set associative on the hash's low
-// word: one lookup reads a set's 8 tags with two 16-B LDS loads and compares full keys only
-// on a tag match, so a wave resolves nearly every row in one step (a linear probe makes the
-// whole wave iterate as long as its longest chain).  A claimer CASes an empty tag 0 ->
-// TAG_BUSY, writes the key, then stores the odd tag; a lane that meets TAG_BUSY in its set
-// reads the set again (the claimer is between two LDS stores).
+// entry (the row then goes to HBM).  The table is 8-way set associative: a set's 8 one-byte
+// tags are one 8-B LDS load, matched against the key's tag with byte-wise zero tests (a few
+// VALU operations for the whole set -- per-tag compares were most of the pass's instructions),
+// and full keys are compared only on a tag match, so a wave resolves nearly every row in one
+// step (a linear probe makes the whole wave iterate as long as its longest chain).  A claimer
+// CASes its empty tag byte 0 -> TAG_BUSY in the set's tag word, writes the key, then turns the
+// byte into the published tag; a lane that meets TAG_BUSY in its set reads the set again (the
+// claimer is between two LDS writes).
 template <int KW>
 __device__ __forceinline__ int at_find_insert(const AggTab<KW> &T, const uint32_t (&k)[KW], uint64_t h, uint32_t maxp) {
-    const uint32_t t = (uint32_t)h | 1u, nsets = T.E >> 3;
+    const uint32_t t8 = 0x80u | ((uint32_t)h & 0x7Fu), t4 = t8 * 0x01010101u, nsets = T.E >> 3;
     uint32_t set = (uint32_t)(((uint64_t)(uint32_t)h * nsets) >> 32);
+    uint32_t *tw = reinterpret_cast<uint32_t *>(T.tag);
     for (uint32_t probes = 0, looks = 0;;) {
         const uint32_t base = set * 8;
         asm volatile("" ::: "memory");   // the set is read afresh on every pass
-        const uint4 t0 = *reinterpret_cast<const uint4 *>(T.tag + base);
-        const uint4 t1 = *reinterpret_cast<const uint4 *>(T.tag + base + 4);
-        const uint32_t tg[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-        uint32_t mt = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) mt |= (tg[j] == t ? 1u : 0u) << j;
-        if (mt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint2 w = *reinterpret_cast<const uint2 *>(T.tag + base);
+        uint64_t mt = (uint64_t)zero_bytes(w.x ^ t4) | (uint64_t)zero_bytes(w.y ^ t4) << 32;
+        if (mt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         while (mt) {   // usually one candidate
-            const uint32_t e = base + (uint32_t)(__builtin_ffs((int)mt) - 1);
+            const uint32_t e = base + ((uint32_t)__builtin_ctzll(mt) >> 3);
             mt &= mt - 1;
             if (at_key_eq<KW>(T, e, k)) return (int)e;
         }
         // not found (a key's first record, or a tag collision): the busy and empty entries --
         // the masks most records (repeats of a key already in the table) never need
-        uint32_t mb = 0, me = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            mb |= (tg[j] == TAG_BUSY ? 1u : 0u) << j;
-            me |= (tg[j] == 0 ? 1u : 0u) << j;
-        }
-        if (mb) {   // a claim in progress in this set: it may be this key
+        if (zero_bytes(w.x ^ 0x01010101u) | zero_bytes(w.y ^ 0x01010101u)) {   // a claim in progress
             if (++looks > SPIN_LIMIT) return -1;   // never expected; the HBM path stays exact
             continue;
         }
+        const uint64_t me = (uint64_t)zero_bytes(w.x) | (uint64_t)zero_bytes(w.y) << 32;
         if (me) {
-            const uint32_t e = base + (uint32_t)(__builtin_ffs((int)me) - 1);
-            if (atomicCAS(&T.tag[e], 0u, TAG_BUSY) == 0u) {
+            const uint32_t bit = (uint32_t)__builtin_ctzll(me), j = bit >> 3, e = base + j;
+            const uint32_t cur = j < 4 ? w.x : w.y, sh = 8 * (j & 3);
+            if (atomicCAS(tw + (e >> 2), cur, cur | (TAG_BUSY << sh)) == cur) {
 #pragma unroll
-                for (int w = 0; w < KW; ++w) T.key[(uint64_t)e * KW + w] = k[w];
-                __hip_atomic_store(&T.tag[e], t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int q = 0; q < KW; ++q) T.key[(uint64_t)e * KW + q] = k[q];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                atomicXor(tw + (e >> 2), (TAG_BUSY ^ t8) << sh);   // BUSY -> the published tag
                 return (int)e;
             }
-            continue;   // lost the entry: read the set again
+            continue;   // the tag word changed under the CAS: read the set again
         }
         if (++probes >= maxp) return -1;   // set full
         set = set + 1 == nsets ? 0 : set + 1;
@@ -958,8 +959,8 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     T.E = E;
     T.first = lds;
     T.agg = lds + E;
-    T.tag = reinterpret_cast<uint32_t *>(lds + (uint64_t)(1 + a.naggs) * E);
-    T.key = T.tag + E;
+    T.tag = reinterpret_cast<uint8_t *>(lds + (uint64_t)(1 + a.naggs) * E);
+    T.key = reinterpret_cast<uint32_t *>(T.tag + E);   // E is a multiple of 8: 8-B aligned
     T.occ_old = T.key + (uint64_t)E * KW;
     T.occ_new = T.occ_old + p.occw;
     T.flag = T.occ_new + p.occw;
@@ -969,7 +970,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     for (;;) {
         if (threadIdx.x == 0) T.flag[1] = atomicAdd(&p.ctl[0], 1u);
         for (uint32_t x = threadIdx.x; x < E; x += PTC) {
-            T.tag[x] = 0;
+            if ((x & 3) == 0) reinterpret_cast<uint32_t *>(T.tag)[x >> 2] = 0;
             T.first[x] = ~0ull;
             for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
         }
@@ -1020,7 +1021,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             __syncthreads();
         }
         for (uint32_t x = threadIdx.x; x < E && !(p.dbg & 16u); x += PTC) {
-            if (!T.tag[x]) continue;
+            if (!(T.tag[x] & 0x80u)) continue;
             uint32_t k[KW];
 #pragma unroll
             for (int q = 0; q < KW; ++q) k[q] = T.key[(uint64_t)x * KW + q];
