@@ -498,6 +498,7 @@ __device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, co
         diff |= q[i].z ^ (4 * i + 2 < KW ? k[4 * i + 2] : 0u);
         diff |= q[i].w ^ (4 * i + 3 < KW ? k[4 * i + 3] : 0u);
     }
+    asm volatile("" : "+v"(diff));   // keep the OR of XORs: LLVM splits `== 0` into per-word compares
     return diff == 0;
 }
 

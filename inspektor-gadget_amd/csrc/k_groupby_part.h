@@ -747,6 +747,7 @@ __device__ __forceinline__ bool at_key_eq(const AggTab<KW> &T, uint32_t e, const
     uint32_t diff = 0;
 #pragma unroll
     for (int w = 0; w < KW; ++w) diff |= d[w] ^ k[w];
+    asm volatile("" : "+v"(diff));   // keep the OR of XORs: LLVM splits `== 0` into per-word compares
     return diff == 0;
 }
 
