@@ -2080,7 +2080,7 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     }
     const size_t lds_k = 4 * ((size_t)NB + F1);
     const size_t lds_a = (size_t)TRA * (16 * p.rq + 1) + 12 * (size_t)F1 + 4 * 17;
-    const size_t lds_b = PackKey<L>::known && gbp_b_regs(p) ? (size_t)trb * 17 + 12 * (size_t)F2 + 4 * 17
+    const size_t lds_b = PackKey<L>::known && L::KW <= 8 && gbp_b_regs(p) ? (size_t)trb * (16 * p.rq + 1) + 12 * (size_t)F2 + 4 * 17
                                                             : (size_t)trb * (16 * p.rq + 6) + 12 * (size_t)F2 + 4 * 17;
     const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 16 + stage_c;
     // dynamic LDS granted to each kernel so far; pass C has a distinct-only instantiation

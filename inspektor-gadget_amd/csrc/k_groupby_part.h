@@ -638,8 +638,87 @@ __global__ __launch_bounds__(1024) void k_gbr_items(PartArgs p) {
 }
 
 // ---- B: a tile of one first-level bucket's records -> its final buckets --------------------
-// pass B's register path (static key layouts, one-quad records; the host sizes its LDS)
-__host__ __device__ inline bool gbp_b_regs(const PartArgs &p) { return p.rq == 1 && p.trb <= 16 * PTA && !(p.dbg & 6u); }
+// pass B's register path (static key layouts, one-quad records; the host sizes its LDS;
+// the template also takes two-quad records, parity-green but not measured faster on C5's
+// partitioned form, so it stays off): each thread holds its records in registers, ranks them there and stages them in
+// LDS already sorted, so the output phase reads position -> bucket -> base like pass A (the
+// LDS-order path reads position -> input index -> bucket -> base)
+__host__ __device__ inline bool gbp_b_regs(const PartArgs &p) {
+    return p.rq == 1 && p.trb <= 16 * PTA && !(p.dbg & 6u);
+}
+
+template <class L, int RQ, int MB>   // MB records per thread (trb <= MB PTA)
+__device__ __forceinline__ void gbp_b_run(const GbArgs &a, const PartArgs &p, uint8_t *lds_raw, const u4v *src,
+                                          uint32_t cnt, uint32_t b1) {
+    constexpr int KW = L::KW;
+    const uint32_t F = 1u << p.f2, trb = p.trb;
+    uint4 *stage = reinterpret_cast<uint4 *>(lds_raw);                   // trb x RQ quads, sorted
+    uint8_t *sb = lds_raw + (size_t)trb * RQ * 16;                       // final bucket of each position
+    uint32_t *hist = reinterpret_cast<uint32_t *>(sb + trb);
+    uint32_t *off = hist + F, *base = off + F, *wsum = base + F;
+    u4v x[MB][RQ];
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+        if (m * PTA + threadIdx.x < cnt) {
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) x[m][q] = __builtin_nontemporal_load(src + (m * PTA + threadIdx.x) * RQ + q);
+        }
+    if (threadIdx.x < F) hist[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t bk[MB], rk[MB];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+        bk[m] = 0xFFFFu;
+        if (m * PTA + threadIdx.x < cnt) {
+            uint32_t w[4 * RQ];
+#pragma unroll
+            for (int q = 0; q < RQ; ++q) {
+                w[4 * q] = x[m][q].x;
+                w[4 * q + 1] = x[m][q].y;
+                w[4 * q + 2] = x[m][q].z;
+                w[4 * q + 3] = x[m][q].w;
+            }
+            uint32_t k[KW];
+            lds_key<L>(p, w, k);
+            bk[m] = hash_bits(hash_key<KW>(k), p.f1, p.f2);
+            rk[m] = atomicAdd(&hist[bk[m]], 1u);
+        }
+    }
+    __syncthreads();
+    const uint32_t c = threadIdx.x < F ? hist[threadIdx.x] : 0u;
+    uint32_t total;
+    const uint32_t o = block_excl_scan(c, wsum, total);
+    if (threadIdx.x < F) {
+        off[threadIdx.x] = o;
+        const uint32_t fb = (b1 << p.f2) + threadIdx.x;
+        base[threadIdx.x] = c ? atomicAdd(p.reg2 ? p.rc2 + fb * p.c2pad : p.cur2 + fb, c) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+        if (bk[m] == 0xFFFFu) continue;
+        const uint32_t pos = off[bk[m]] + rk[m];
+#pragma unroll
+        for (int q = 0; q < RQ; ++q) stage[pos * RQ + q] = make_uint4(x[m][q].x, x[m][q].y, x[m][q].z, x[m][q].w);
+        sb[pos] = (uint8_t)bk[m];
+    }
+    __syncthreads();
+    uint4 *out = reinterpret_cast<uint4 *>(p.recs2);
+    const uint32_t nq = cnt * RQ;
+    for (uint32_t q0 = threadIdx.x & ~63u; q0 < nq; q0 += PTA) {   // wave-uniform trip count
+        const uint32_t qi = q0 + (threadIdx.x & 63);
+        const bool live = qi < nq;
+        const uint32_t jj = qi / RQ, q = qi % RQ;
+        const uint32_t b = live ? sb[jj] : 0u;
+        const uint32_t g = base[b] + jj - off[b];
+        bool spill = false;
+        if (!live) {
+        } else if (!p.reg2) out[(uint64_t)g * RQ + q] = stage[qi];
+        else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * RQ + q] = stage[qi];
+        else spill = q == 0;
+        if (p.reg2) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? jj : 0u) * RQ));
+    }
+}
 
 // B tile `blockIdx.x` = records [j * trb, (j + 1) * trb) of first-level bucket b1 in recs1
 // (contiguous): loaded flat into LDS (coalesced), ranked by the next f2 hash bits with LDS
@@ -665,66 +744,9 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
                               : min(p.start2[(b1 + 1) << p.f2], s + trb);
     const uint32_t cnt = e - s;
     const u4v *src = reinterpret_cast<const u4v *>(p.recs1) + (uint64_t)s * rq;
-    if constexpr (PackKey<L>::known) {
+    if constexpr (PackKey<L>::known && L::KW <= 8) {   // (wider keys never have 1-2 quad records)
         if (gbp_b_regs(p)) {
-            // one-quad records of a static key layout: each thread holds its records in
-            // registers, ranks them there and stages them in LDS already sorted, so the
-            // output phase reads position -> bucket -> base like pass A (the LDS-order path
-            // below reads position -> input index -> bucket -> base)
-            constexpr int MB = 16;   // records per thread (trb <= 16 PTA)
-            uint8_t *sb = lds_raw + (size_t)trb * 16;   // final bucket of each sorted position
-            uint32_t *h2 = reinterpret_cast<uint32_t *>(sb + trb);
-            uint32_t *of2 = h2 + F, *ba2 = of2 + F, *ws2 = ba2 + F;
-            u4v x[MB];
-#pragma unroll
-            for (int m = 0; m < MB; ++m)
-                if (m * PTA + threadIdx.x < cnt) x[m] = __builtin_nontemporal_load(src + m * PTA + threadIdx.x);
-            if (threadIdx.x < F) h2[threadIdx.x] = 0;
-            __syncthreads();
-            uint32_t bk[MB], rk[MB];
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                bk[m] = 0xFFFFu;
-                if (m * PTA + threadIdx.x < cnt) {
-                    const uint32_t w[4] = {x[m].x, x[m].y, x[m].z, x[m].w};
-                    uint32_t k[KW];
-                    lds_key<L>(p, w, k);
-                    bk[m] = hash_bits(hash_key<KW>(k), p.f1, p.f2);
-                    rk[m] = atomicAdd(&h2[bk[m]], 1u);
-                }
-            }
-            __syncthreads();
-            const uint32_t c = threadIdx.x < F ? h2[threadIdx.x] : 0u;
-            uint32_t total;
-            const uint32_t o = block_excl_scan(c, ws2, total);
-            if (threadIdx.x < F) {
-                of2[threadIdx.x] = o;
-                const uint32_t fb = (b1 << p.f2) + threadIdx.x;
-                ba2[threadIdx.x] = c ? atomicAdd(p.reg2 ? p.rc2 + fb * p.c2pad : p.cur2 + fb, c) : 0u;
-            }
-            __syncthreads();
-            uint4 *stage2 = reinterpret_cast<uint4 *>(lds_raw);
-#pragma unroll
-            for (int m = 0; m < MB; ++m) {
-                if (bk[m] == 0xFFFFu) continue;
-                const uint32_t pos = of2[bk[m]] + rk[m];
-                stage2[pos] = make_uint4(x[m].x, x[m].y, x[m].z, x[m].w);
-                sb[pos] = (uint8_t)bk[m];
-            }
-            __syncthreads();
-            uint4 *out = reinterpret_cast<uint4 *>(p.recs2);
-            for (uint32_t q0 = threadIdx.x & ~63u; q0 < cnt; q0 += PTA) {   // wave-uniform trip count
-                const uint32_t jj = q0 + (threadIdx.x & 63);
-                const bool live = jj < cnt;
-                const uint32_t b = live ? sb[jj] : 0u;
-                const uint32_t g = ba2[b] + jj - of2[b];
-                bool spill = false;
-                if (!live) {
-                } else if (!p.reg2) out[g] = stage2[jj];
-                else if (g < p.reg2) out[(uint64_t)((b1 << p.f2) + b) * p.reg2 + g] = stage2[jj];
-                else spill = true;
-                if (p.reg2) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage2 + (live ? jj : 0u)));
-            }
+            gbp_b_run<L, 1, 16>(a, p, lds_raw, src, cnt, b1);
             return;
         }
     }
