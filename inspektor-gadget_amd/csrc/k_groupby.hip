@@ -1987,27 +1987,37 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     if (4 * p.rq > (uint32_t)part_w<KW, NV>()) return igx_fail(ctx, IGX_EINVAL, "groupby_update: record layout");
     // final buckets: enough that a bucket's share of the capacity fills at most ~60% of the
     // C block's LDS table; each bucket owns whole probe regions of the table
-    const size_t entry = agg_entry_bytes(KW, t->naggs);
+    // pass C's packed entries (c_row_pe): distinct-only, a static key of <= 3 packed words,
+    // row-offset indices; IGX_GBP_NOPE=1 keeps the general table (A/B)
+    p.pe = pack_words<L>() <= 3 && t->naggs == 0 && p.iw == 1 &&
+           !std::getenv("IGX_GBP_COMBINE") && !std::getenv("IGX_GBP_NOPE");
+    const size_t entry = p.pe ? 17 : agg_entry_bytes(KW, t->naggs);
     p.uc = p.rq <= 1 ? 2 : 1;
     if (const char *d = std::getenv("IGX_GBP_UC"))   // tuning knob: records per thread and round of pass C
         p.uc = std::max<uint32_t>(1, std::min<uint32_t>(UCMAX, (uint32_t)std::strtoul(d, nullptr, 0)));
     const size_t stage_c = (size_t)p.uc * PTC * p.rq * 16;
     const uint32_t lb_max = std::min<uint32_t>(PART_LB_MAX, t->sbits - t->rbits);
-    auto entries = [&](uint32_t lb) {
+    auto entries = [&](uint32_t lb, size_t esz) {
         const int64_t occw = (int64_t)1 << (t->sbits - lb - 5);
         const int64_t room = (int64_t)PART_AGG_LDS - (int64_t)stage_c - 8 * occw - 16;
-        if (room < (int64_t)(8 * entry)) return 0u;
+        if (room < (int64_t)(8 * esz)) return 0u;
         // whole 8-way sets, E a multiple of 16: the byte tags keep what follows them 16-B aligned
-        return (uint32_t)std::min<int64_t>(65520, room / (int64_t)entry) & ~15u;
+        return (uint32_t)std::min<int64_t>(65520, room / (int64_t)esz) & ~15u;
     };
+    // the bucket count follows the general entry size, so packed entries only lower the load
+    // factor (IGX_GBP_PE_LB=1: let them halve the bucket count instead)
+    const size_t lb_entry = std::getenv("IGX_GBP_PE_LB") ? entry : agg_entry_bytes(KW, t->naggs);
     uint32_t lb = 0;
-    while (lb < lb_max && (double)(t->cap >> lb) > 0.9 * entries(lb)) ++lb;
+    while (lb < lb_max && (double)(t->cap >> lb) > 0.9 * entries(lb, lb_entry)) ++lb;
     p.lb = lb;
     p.f1 = (lb + 1) / 2;
-    p.f2 = lb / 2;
+    if (const char *d = std::getenv("IGX_GBP_F1"))   // tuning knob: first-level bucket bits
+        p.f1 = std::min<uint32_t>(std::min<uint32_t>(lb, 8u), (uint32_t)std::strtoul(d, nullptr, 0));
+    p.f1 = std::max<uint32_t>(p.f1, lb > 8 ? lb - 8 : 0u);   // both levels <= 256 buckets
+    p.f2 = lb - p.f1;
     p.sb_log = t->sbits - lb;
     p.occw = 1u << (p.sb_log - 5);
-    p.E = entries(lb);
+    p.E = entries(lb, entry);
     if (p.E < 16) return igx_fail(ctx, IGX_ENOTSUP, "groupby_update: key of %u words too wide for the partitioned form", KW);
     if (const char *d = std::getenv("IGX_GBP_ENTRIES"))   // tests: a small LDS table overflows
         p.E = std::max<uint32_t>(16, std::min<uint32_t>(p.E, (uint32_t)std::strtoul(d, nullptr, 0))) & ~15u;

@@ -97,6 +97,7 @@ struct PartArgs {
     uint32_t reg1, reg2;       // records per first-level slice / final region (0: exact runs)
     uint32_t s1log;            // log2 slices per first-level region (0 in the exact form)
     uint32_t c2pad;            // words between two final-region cursors (rc2)
+    uint32_t pe;               // pass C keeps 16-B packed entries (distinct-only, see c_row_pe)
 };
 
 // record words (compile-time bound): packed key words, loaded columns, index
@@ -185,6 +186,12 @@ struct PackKey<L, true> {
     static constexpr bool known = true;
     static constexpr PackTab T = pack_static<L>();
 };
+// packed key words of a static layout (a large number for the runtime layouts)
+template <class L>
+__host__ __device__ constexpr uint32_t pack_words() {
+    if constexpr (PackKey<L>::known) return PackKey<L>::T.kpn;
+    else return 0xFFu;
+}
 
 // A record lives in LDS as rq x 4 words while it is built or read: its fields sit at
 // runtime word offsets (host-chosen layout), so LDS addressing does the packing and no
@@ -1038,6 +1045,83 @@ __device__ __forceinline__ void c_row(const GbArgs &a, const PartArgs &p, const 
     }
 }
 
+// Packed entries (distinct-only tables of static layouts whose key packs into at most 3
+// words, events indexed by their row offset): an LDS entry is ONE 16-B word {packed key
+// words, first row offset}, so a repeat of a known key costs the set's tag load and one
+// entry load -- key compare and first index together -- instead of a key load and a
+// separate first-index load, and an entry takes 17 B of LDS instead of 25 (more entries per
+// bucket).  Same byte tags and claim protocol as at_find_insert.
+template <int PW>
+__device__ __forceinline__ int pe_find_insert(uint8_t *tg8, uint4 *ent, uint32_t E, const uint32_t (&kp)[PW],
+                                              uint32_t h, uint32_t idx, uint32_t maxp, uint32_t &fst) {
+    const uint32_t t8 = 0x80u | (h & 0x7Fu), t4 = t8 * 0x01010101u, nsets = E >> 3;
+    uint32_t set = (uint32_t)(((uint64_t)h * nsets) >> 32);
+    uint32_t *tw = reinterpret_cast<uint32_t *>(tg8);
+    for (uint32_t probes = 0, looks = 0;;) {
+        const uint32_t base = set * 8;
+        asm volatile("" ::: "memory");   // the set is read afresh on every pass
+        const uint2 w = *reinterpret_cast<const uint2 *>(tg8 + base);
+        uint64_t mt = (uint64_t)zero_bytes(w.x ^ t4) | (uint64_t)zero_bytes(w.y ^ t4) << 32;
+        if (mt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        while (mt) {
+            const uint32_t e = base + ((uint32_t)__builtin_ctzll(mt) >> 3);
+            mt &= mt - 1;
+            const uint4 q = ent[e];
+            uint32_t diff = q.x ^ kp[0];
+            if constexpr (PW > 1) diff |= q.y ^ kp[1];
+            if constexpr (PW > 2) diff |= q.z ^ kp[2];
+            asm volatile("" : "+v"(diff));
+            if (diff == 0) {
+                fst = q.w;
+                return (int)e;
+            }
+        }
+        if (zero_bytes(w.x ^ 0x01010101u) | zero_bytes(w.y ^ 0x01010101u)) {   // a claim in progress
+            if (++looks > SPIN_LIMIT) return -1;
+            continue;
+        }
+        const uint64_t me = (uint64_t)zero_bytes(w.x) | (uint64_t)zero_bytes(w.y) << 32;
+        if (me) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(me) >> 3, e = base + j;
+            const uint32_t cur = j < 4 ? w.x : w.y, sh = 8 * (j & 3);
+            if (atomicCAS(tw + (e >> 2), cur, cur | (TAG_BUSY << sh)) == cur) {
+                ent[e] = make_uint4(kp[0], PW > 1 ? kp[PW > 1 ? 1 : 0] : 0u, PW > 2 ? kp[PW > 2 ? 2 : 0] : 0u, idx);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                atomicXor(tw + (e >> 2), (TAG_BUSY ^ t8) << sh);
+                fst = idx;
+                return (int)e;
+            }
+            continue;
+        }
+        if (++probes >= maxp) return -1;
+        set = set + 1 == nsets ? 0 : set + 1;
+    }
+}
+
+template <class L>
+__device__ __forceinline__ void c_row_pe(const GbArgs &a, const PartArgs &p, uint8_t *tg8, uint4 *ent, uint32_t E,
+                                         uint32_t *flag, bool ok, const uint32_t *rec) {
+    constexpr int PW = (int)pack_words<L>();
+    constexpr int KW = L::KW;
+    uint32_t kp[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) kp[j] = rec[j];
+    const uint32_t idx = rec[p.ipos];
+    const uint32_t hh = (uint32_t)lds_hash<PW>(kp);
+    if (!ok || (p.dbg & 32u)) return;
+    uint32_t fst = 0;
+    const int ei = pe_find_insert<PW>(tg8, ent, E, kp, hh, idx, p.maxp, fst);
+    if (ei >= 0) {
+        if (idx < fst) atomicMin(reinterpret_cast<uint32_t *>(ent + ei) + 3, idx);
+    } else {
+        flag[0] = 1;
+        uint32_t k[KW];
+        lds_key<L>(p, rec, k);
+        const uint64_t v[1] = {0};
+        hbm_merge<KW, 1>(a, k, hash_key<KW>(k), v, a.base_idx + idx);
+    }
+}
+
 template <class L, int NV, int NA>
 __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
@@ -1053,6 +1137,16 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     T.occ_old = T.key + (uint64_t)E * KW;
     T.occ_new = T.occ_old + p.occw;
     T.flag = T.occ_new + p.occw;
+    constexpr bool PEC = NA == 0 && pack_words<L>() <= 3;
+    const bool pe = PEC && p.pe;
+    uint8_t *tg8 = reinterpret_cast<uint8_t *>(lds);     // packed entries: E tag bytes ...
+    uint4 *ent = reinterpret_cast<uint4 *>(tg8 + E);      // ... then E 16-B entries
+    if (pe) {
+        T.tag = tg8;
+        T.occ_old = reinterpret_cast<uint32_t *>(ent + E);
+        T.occ_new = T.occ_old + p.occw;
+        T.flag = T.occ_new + p.occw;
+    }
     uint4 *stage = reinterpret_cast<uint4 *>(T.flag + 4);   // RC x rq quads (16-B aligned: see the launch)
     const u4v *recs = reinterpret_cast<const u4v *>(p.recs2);
     const uint32_t nitems = p.ctl[2];
@@ -1060,6 +1154,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         if (threadIdx.x == 0) T.flag[1] = atomicAdd(&p.ctl[0], 1u);
         for (uint32_t x = threadIdx.x; x < E; x += PTC) {
             if ((x & 3) == 0) reinterpret_cast<uint32_t *>(T.tag)[x >> 2] = 0;
+            if (pe) continue;   // a claim writes its whole entry
             T.first[x] = ~0ull;
             for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
         }
@@ -1094,7 +1189,14 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             if (r0 + RC < e) prefetch(r0 + RC);
             for (uint32_t u = 0; u < uc; ++u) {
                 const uint32_t i = u * PTC + threadIdx.x;
-                c_row<L, NA>(a, p, T, r0 + i < e, reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq));
+                const uint32_t *rec = reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq);
+                if constexpr (PEC) {
+                    if (pe) {
+                        c_row_pe<L>(a, p, tg8, ent, E, T.flag, r0 + i < e, rec);
+                        continue;
+                    }
+                }
+                c_row<L, NA>(a, p, T, r0 + i < e, rec);
             }
         }
         __syncthreads();
@@ -1111,6 +1213,19 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         }
         for (uint32_t x = threadIdx.x; x < E && !(p.dbg & 16u); x += PTC) {
             if (!(T.tag[x] & 0x80u)) continue;
+            if constexpr (PEC) {
+                if (pe) {
+                    const uint4 q = ent[x];
+                    const uint32_t w4[4] = {q.x, q.y, q.z, 0u};
+                    uint32_t k[KW];
+                    lds_key<L>(p, w4, k);
+                    const uint64_t v[1] = {0};
+                    const uint64_t h = hash_key<KW>(k), f = a.base_idx + q.w;
+                    if (owned) flush_owned<KW, 1>(a, T, k, h, v, f, sb, p.sb_log);
+                    else hbm_merge<KW, 1>(a, k, h, v, f);
+                    continue;
+                }
+            }
             uint32_t k[KW];
 #pragma unroll
             for (int q = 0; q < KW; ++q) k[q] = T.key[(uint64_t)x * KW + q];
