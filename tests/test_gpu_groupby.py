@@ -347,6 +347,9 @@ def test_netpolicy_mark_and_masked_distinct(oracle, E, H, igx, torch):
     keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
     ref_keep = oracle.np_mark(ev_h)
     assert np.array_equal(H.host(keep).astype(bool), ref_keep)
+    # columns at an offset (u8 columns 4-B but not 16-B aligned)
+    keep4 = E.np_mark(ev["type"][4:], ev["pkt"][4:], ev["hostip"][4:], ev["raddr"][4:])
+    assert np.array_equal(H.host(keep4).astype(bool), ref_keep[4:])
     names = ("src", "pkt", "peer", "port")
     tab = E.Table([4, 1, 4, 2], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], n)
     tab.update([ev[k] for k in names], [0, 1, 2, 3], n, 17, valid=keep)
