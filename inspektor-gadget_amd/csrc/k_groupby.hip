@@ -758,7 +758,7 @@ constexpr uint32_t WHAT_MIN = 15;           // entry kind: atomicMin on `first`
 // wave roles in a workgroup: a.nl loaders stream rows, the next 15 - a.nl waves (probers)
 // resolve LDS misses against HBM, and the last wave serves the HBM-update ring
 constexpr uint32_t NWAVES = GTB / 64;
-constexpr uint32_t NL_DEFAULT = 8;    // loader waves (7 probers + 1 server): tools/gpu/nl_cfg.sh
+constexpr uint32_t NL_DEFAULT = 8;    // loader waves (7 probers + 1 server); IGX_GB_LOADERS sweeps
 
 struct Ring {
     uint2 *lo;            // {slot, (lap << 4) | what}
@@ -1696,6 +1696,7 @@ struct igx_table {
     uint64_t *n_groups = nullptr;
     uint64_t rows_fed = 0;       // rows given to update since the last reset
     bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
+    bool more_probers = false;   // ... on more than MORE_PROBERS_PCT % of its rows
     uint32_t mode = IGX_GB_AUTO; // igx_groupby_set_mode
     uint32_t direct_left = 0;    // AUTO: intervals to run in the direct form before re-measuring
     uint32_t region_off = 0;     // AUTO: intervals to partition exactly after a region overflowed
@@ -1899,6 +1900,7 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
 
 constexpr size_t GB_LDS_TOTAL = 156 * 1024;    // cache + the two rings (dynamic LDS)
 constexpr uint64_t DIRECT_MISS_PCT = 90;        // AUTO: LDS-miss share that selects the partitioned form
+constexpr uint64_t MORE_PROBERS_PCT = 40;       // LDS-miss share above which a loader wave becomes a prober
 constexpr uint32_t DIRECT_RUN = 16;             // ... for this many intervals
 
 template <class L, bool DBG, int NA>
@@ -2480,7 +2482,10 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.rmask = (1ull << t->rbits) - 1;
     a.max_probe = 1u << t->rbits;
     if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
-    a.nl = NL_DEFAULT;
+    // one loader wave fewer (one prober more) when the last interval missed the cache on
+    // more than MORE_PROBERS_PCT % of its rows: C5 (≈42 % misses) 6.15 -> 5.95-6.02 ms with 7
+    // loaders, C2 (≈35 %) 3.69 -> 3.86 ms, so C2 keeps 8
+    a.nl = t->more_probers ? NL_DEFAULT - 1 : NL_DEFAULT;
     if (const char *d = std::getenv("IGX_GB_LOADERS")) {   // tuning knob
         const unsigned long v = std::strtoul(d, nullptr, 0);
         if (v >= 1 && v <= NWAVES - 2) a.nl = (uint32_t)v;
@@ -2605,6 +2610,7 @@ static int fin_apply(igx_table *t) {
     // row; C4: 4.1 vs 4.4 ms direct, 6.4 ms cached), then one cached interval to measure again.
     if (f.rows_fed >= 1000000 && !f.direct && !f.part) {
         t->prefer_sm = misses * 10 > f.rows_fed * 7;
+        t->more_probers = misses * 100 > f.rows_fed * MORE_PROBERS_PCT;
         if (t->mode == IGX_GB_AUTO && misses * 100 > f.rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }
     if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
