@@ -106,11 +106,17 @@ class IgxComm:
         from . import _abi
         rank, ws = d.get_rank(), d.get_world_size()
         uid = (C.c_uint8 * _abi.DIST_ID_BYTES)()
+        ok = 1
         if rank == 0:
-            self.ctx.check(L.igx_dist_get_unique_id(uid))
-        t = torch.tensor(list(uid), dtype=torch.uint8, device=torch.device("cuda", self.ctx.device))
+            ok = int(L.igx_dist_get_unique_id(uid) == 0)
+        # every rank joins the broadcast, a failed id included (its last byte says so), so no
+        # rank is left waiting in it while rank 0 moves on to the next collective
+        t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=torch.device("cuda", self.ctx.device))
         d.broadcast(t, 0)
-        uid = (C.c_uint8 * _abi.DIST_ID_BYTES)(*t.cpu().tolist())
+        v = t.cpu().tolist()
+        if not v[-1]:
+            raise RuntimeError("igx_dist_get_unique_id failed on rank 0")
+        uid = (C.c_uint8 * _abi.DIST_ID_BYTES)(*v[:-1])
         h = C.c_void_p()
         self.ctx.check(L.igx_dist_init(self.ctx.h, uid, ws, rank, C.byref(h)))
         self.h = h

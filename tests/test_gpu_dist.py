@@ -97,3 +97,29 @@ def test_igx_dist_rccl_single_rank(igx, torch, oracle):
         assert L.igx_dist_barrier(h) == A.IGX_EIO
     finally:
         ctx.check(L.igx_dist_destroy(h))
+
+
+def test_igx_comm_transport_single_rank():
+    """dist.IgxComm (the bench's N > 1 transport) built through a real one-rank "nccl" group:
+    rank 0's unique id + status byte broadcast, igx_dist_init, an all-reduce, close -- in a
+    child process so the process group does not outlive the test."""
+    code = (
+        "import os, sys, torch, torch.distributed as d\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import importlib; igx = importlib.import_module('inspektor-gadget_amd')\n"
+        "from importlib import import_module\n"
+        "dist = import_module('inspektor-gadget_amd.dist')\n"
+        "torch.cuda.set_device(0)\n"
+        "d.init_process_group('nccl', rank=0, world_size=1)\n"
+        "c = dist.IgxComm(d)\n"
+        "h = torch.arange(27 * 4, dtype=torch.int32, device='cuda').view(torch.uint32).view(4, 27)\n"
+        "ref = h.clone()\n"
+        "c.allreduce_u32(h)\n"
+        "torch.cuda.synchronize()\n"
+        "assert torch.equal(h.view(torch.int32), ref.view(torch.int32))\n"
+        "c.close()\n"
+        "d.destroy_process_group()\n"
+        "print('igx comm ok')\n")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "igx comm ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
