@@ -22,6 +22,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline`
 group-by kernel (HIP events on the stream it runs on) and `cpu_baseline` (the oracle's
 restatement of the reference's CPU path on a bounded sample, all host cores, with the
 single-thread number beside it; rank 0, N=1).
+
+After each config's timed loop (outside the timed region) the LAST timed interval's output --
+the very tables, histogram and top-K the measured steps produced -- is checked against the
+oracle on the same stream (`check` in each config, `check` at the top level for C2; default on,
+`--no-check` skips it).  A mismatch makes the process exit 3 after the line is printed.
 """
 import argparse
 import importlib
@@ -66,7 +71,7 @@ def c5_oracle_aggs(h):
             {"kind": "sum", "val": h["count"], "cond": h["op"], "cond_val": 1}]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -82,13 +87,15 @@ def parse():
     p.add_argument("--config-events", type=int, default=125_000_000,
                    help="events per GPU for C3/C4/C5 (the 8-GPU configs' 1B / 8)")
     p.add_argument("--config-steps", type=int, default=5)
-    p.add_argument("--check", action="store_true", help="verify the top-K against the oracle")
-    p.add_argument("--transport", choices=("igx", "torch"), default="igx",
-                   help="N>1 exchanges: the igx_dist_* C ABI over RCCL (falls back to torch's "
-                        "collectives if igx_dist_init fails on any rank) or torch's collectives")
+    p.add_argument("--no-check", dest="check", action="store_false",
+                   help="skip the post-run check of each config's last timed interval against the oracle")
+    p.add_argument("--transport", choices=("igx", "torch"), default="torch",
+                   help="N>1 exchanges: torch's collectives (RCCL on the nccl group; the default until "
+                        "the igx_dist_* send/recv loops have run with two or more GPUs) or the igx_dist_* "
+                        "C ABI over RCCL (falls back to torch's if igx_dist_init fails on any rank)")
     p.add_argument("--launch-dry-run", action="store_true",
                    help="launcher self-test: each rank prints its RANK/WORLD_SIZE and exits, no GPU")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def free_port():
@@ -226,6 +233,108 @@ def cpu_entry(units, single, multi, threads, unit, sample):
 
 
 # ------------------------------------------------------------------------------------
+# post-run parity checks (outside every timed region; the oracle is the checker only)
+# ------------------------------------------------------------------------------------
+def check_threads(ctx):
+    """Host threads for one rank's oracle check: the rank's share of the CPUs it may use
+    (a launcher may set OMP_NUM_THREADS=1, which would make a 100M-event check crawl)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(32, n // max(1, ctx["world"])))
+
+
+def u64_col(rows, off):
+    return rows[:, off:off + 8].copy().view(np.uint64).ravel()
+
+
+def tcp_fields66(rows):
+    """Device packed ip_key_t (each column padded to 4 B: saddr 0:16 daddr 16:32 mntns 32:40
+    pid 40:44 comm 44:60 lport 60:62 dport 64:66 family 68:70) -> the 66 field bytes."""
+    return np.concatenate([rows[:, 0:62], rows[:, 64:66], rows[:, 68:70]], axis=1)
+
+
+def topk_equal(cand_rows, off_aggs, off_first, first, aggs):
+    """A device top-K (packed rows) against the oracle's (first (k,), aggs [(k,)...])."""
+    if cand_rows.shape[0] != len(first):
+        return False
+    if not np.array_equal(u64_col(cand_rows, off_first), np.asarray(first, np.uint64)):
+        return False
+    return all(np.array_equal(u64_col(cand_rows, o), np.asarray(a, np.uint64)) for o, a in zip(off_aggs, aggs))
+
+
+def gather_checks(ctx, obj):
+    """Every rank's check record on every rank (torch all_gather_object: the check does not
+    ride the product's own transport)."""
+    if ctx["world"] == 1:
+        return [obj]
+    out = [None] * ctx["world"]
+    ctx["dist"].all_gather_object(out, obj)
+    return out
+
+
+def check_c2(a, ctx, tab, cand, cdf_h, Gn):
+    """C2's last timed interval vs or_top_tcp_mt on the same stream: this rank's group count
+    and whole-table checksum (key fields, sent, recv, first index of every group), and the
+    top-20 (first, sent, recv) -- at N>1 the global top-20 against the oracle's merge of every
+    rank's top-20 (rank-disjoint key universes; the position is the global first index)."""
+    torch, E, H, O = ctx["torch"], ctx["E"], ctx["H"], ctx["O"]
+    rank, world = ctx["rank"], ctx["world"]
+    N, G, K = a.events, a.keys, a.topk
+    rows = H.host(table_rows(E, torch, tab, tab.fin))
+    dev_cs = O.tcp_group_checksum(tcp_fields66(rows), u64_col(rows, 72), u64_col(rows, 80), u64_col(rows, 88))
+    del rows
+    h = O.gen_tcp(0xC2, rank, G, cdf_h, rank * N, N)
+    Gref, sent, recv, first, cs = O.top_tcp_mt(h, K, base_idx=rank * N, threads=check_threads(ctx), checksum=True)
+    del h
+    recs = gather_checks(ctx, {"groups": int(Gn), "oracle_groups": int(Gref), "checksum_equal": dev_cs == cs,
+                               "sent": sent, "recv": recv, "first": first})
+    if rank != 0:
+        return None
+    S = np.concatenate([r["sent"] for r in recs])
+    R = np.concatenate([r["recv"] for r in recs])
+    F = np.concatenate([r["first"] for r in recs])
+    order = np.argsort(F, kind="stable")              # pre-sort position = global first index
+    perm = O.go_sort_entries([(S[order], "uint64", True), (R[order], "uint64", True)], len(F))
+    sel = order[perm[:K].astype(np.int64)]
+    c = H.host(cand)
+    top_ok = topk_equal(c, (72, 80), 88, F[sel], (S[sel], R[sel]))
+    groups_ok = all(r["groups"] == r["oracle_groups"] for r in recs)
+    cs_ok = all(r["checksum_equal"] for r in recs)
+    return {"bit_exact": bool(groups_ok and cs_ok and top_ok), "groups_equal": bool(groups_ok),
+            "table_checksum_equal": bool(cs_ok), "topk_equal": bool(top_ok),
+            "groups": [r["groups"] for r in recs], "oracle_groups": [r["oracle_groups"] for r in recs],
+            "what": "last timed interval vs oracle or_top_tcp_mt on the same stream: per-rank group count and "
+                    "whole-table checksum (66 key bytes + sent + recv + first of every group), global top-"
+                    f"{K} (first, sent, recv)" + (" vs the oracle merge of every rank's top-K" if world > 1 else "")}
+
+
+def check_table(a, ctx, tab, cand, keys_h, oaggs, valid, naggs, sort, K):
+    """C4 / C5 (N=1): the last timed interval's table -- group count and a checksum of every
+    (key, aggregates, first index) -- and, with `sort`, its top-K against or_groupby_topk_mt."""
+    torch, E, H, O = ctx["torch"], ctx["E"], ctx["H"], ctx["O"]
+    fin = tab.fin
+    rows = H.host(table_rows(E, torch, tab, fin))
+    kb = fin["key_bytes"]
+    dev_cs = O.group_checksum(rows[:, :kb], [u64_col(rows, kb + 8 * x) for x in range(naggs)],
+                              u64_col(rows, kb + 8 * naggs))
+    ng = rows.shape[0]
+    del rows
+    Gref, first, aggs, cs = O.groupby_topk_mt(keys_h, oaggs, valid=valid, sort=sort, k=K,
+                                              threads=check_threads(ctx), checksum=True)
+    out = {"groups": int(fin["n_groups"]), "oracle_groups": int(Gref), "groups_equal": fin["n_groups"] == Gref == ng,
+           "table_checksum_equal": dev_cs == cs}
+    ok = out["groups_equal"] and out["table_checksum_equal"]
+    if sort:
+        out["topk_equal"] = topk_equal(H.host(cand), [kb + 8 * x for x in range(naggs)], kb + 8 * naggs,
+                                       first, [aggs[:, x] for x in range(naggs)])
+        ok = ok and out["topk_equal"]
+    out["bit_exact"] = bool(ok)
+    return {k: (bool(v) if isinstance(v, (bool, np.bool_)) else v) for k, v in out.items()}
+
+
+# ------------------------------------------------------------------------------------
 # C2: the headline
 # ------------------------------------------------------------------------------------
 def family_in_pred(A, col):
@@ -282,15 +391,8 @@ def run_c2(a, ctx):
                                 f"{EV_BYTES} B/event x events + {GROUP_BYTES} B/group x groups", "c2",
                                 {"events": N, "keys": G, "zipf": a.zipf})}
     out["roofline"]["hbm_pct_of_peak_whole_step"] = 100.0 * alg / (out["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS
-    if a.check and rank == 0 and world == 1:
-        O = ctx["O"]
-        evh = O.gen_tcp(0xC2, 0, G, cdf_h, 0, N)
-        Gref, _, sent, recv, first = O.top_tcp(evh, K)
-        c = H.host(st["cand"])
-        ok = (np.array_equal(c[:, 88:96].copy().view(np.uint64).ravel(), first)
-              and np.array_equal(c[:, 72:80].copy().view(np.uint64).ravel(), sent)
-              and np.array_equal(c[:, 80:88].copy().view(np.uint64).ravel(), recv))
-        out["check"] = {"oracle_groups": int(Gref), "groups": int(Gn), "topk_bit_exact": bool(ok)}
+    if a.check:
+        out["check"] = check_c2(a, ctx, tab, st["cand"], cdf_h, Gn)
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = a.cpu_sample
@@ -340,6 +442,21 @@ def run_c1(a, ctx):
            "ms_per_step": ms, "selected": sel,
            "hbm_pct_of_peak_whole_step": 100.0 * alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
            "note": "launch- and sync-bound at 1M rows (several kernels, one host sync per filter)"}
+    if a.check and ctx["rank"] == 0:
+        # the last timed step's view: its selection vector, in SortEntries order, against the
+        # oracle's FilterEntries (one or_filter per filter, filter.go:294-325) + SortEntries
+        # (Go SliceStable per key, sort.go:35-83) of this rank's batch
+        O = ctx["O"]
+        h = O.gen_open(0xC1, O.zipf_cdf(64, 1.0), ctx["rank"] * n, n)
+        ocols = {"err": O.OCol("err", "int64", 8), "pid": O.OCol("pid", "uint32", 4)}
+        osel = O.filter_entries(ocols, {"err": h["err"], "pid": h["pid"]}, None, filters)
+        perm = O.go_sort_entries([(h["comm"][osel], "string", False), (h["pid"][osel], "uint32", True)], len(osel))
+        want = osel[perm.astype(np.int64)]
+        got = H.host(st["out"].sel).astype(np.int64) if st["out"].sel is not None else np.arange(sel)
+        ok = bool(np.array_equal(got, want))
+        out["check"] = {"bit_exact": ok, "selected": int(sel), "oracle_selected": int(len(want)),
+                        "what": "rank 0's last timed step: selected row ids in output order vs oracle "
+                                "filter_entries + go_sort_entries"}
     if ctx["rank"] == 0 and ctx["world"] == 1 and a.cpu_sample:
         O = ctx["O"]
         h = O.gen_open(0xC1, O.zipf_cdf(64, 1.0), 0, n)
@@ -388,6 +505,19 @@ def run_c3(a, ctx):
            "roofline": roofline(alg, clk.avg(), "k_hist", "16 B/event (dev 4, cont 4, delta 8) + 442 KB out",
                                 "c3", {"events": n}),
            "total_counted": int(H.host(hist).astype(np.uint64).sum())}
+    if a.check:
+        # the last timed step's histogram (all-reduced at N>1) vs the sum of every rank's
+        # oracle histogram (or_hist_log2_mt: biolatency.bpf.c:100-154 per event)
+        O = ctx["O"]
+        hh = O.gen_bio(0xC3, q, rank * n, n)
+        ref = O.hist_log2_mt(hh["dev"], hh["cont"], hh["delta"], devs, C3_NCONT, threads=check_threads(ctx))
+        del hh
+        refs = gather_checks(ctx, ref)
+        if rank == 0:
+            tot = np.sum([r.astype(np.uint64) for r in refs], axis=0).astype(np.uint32)   # u32 wrap like the device
+            ok = bool(np.array_equal(H.host(hist), tot))
+            out["check"] = {"bit_exact": ok, "what": "last timed step's whole u32[4096][27] histogram vs the sum "
+                                                     f"of {world} rank(s)' oracle histograms"}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 40_000_000
@@ -453,6 +583,18 @@ def run_c4(a, ctx):
                                 "24 B/event (src 4, peer 4, port 2, pkt 1, type 1, proto 1, hostip 4, raddr 4, "
                                 "+3 pad) + 20 B/distinct tuple (key 12 + first 8)", "c4", {"events": n})}
     out["roofline"]["alg_bytes_per_launch"] = alg
+    if a.check and world == 1:
+        O = ctx["O"]
+        h = O.gen_np(*C4_GEN, 0, n)
+        keys, valid = O.pad_keys(h, names), O.np_mark(h)
+        del h
+        out["check"] = check_table(a, ctx, tab, None, keys, [], valid, 0, (), 0)
+        out["check"]["what"] = ("last timed interval's table vs oracle or_groupby_topk_mt distinct on the same "
+                                "stream: distinct count + checksum of every (tuple, first index)")
+        del keys, valid
+    elif a.check and rank == 0:
+        out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
+                                   "tests/test_gpu_dist.py"}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 20_000_000
@@ -535,6 +677,18 @@ def run_c5(a, ctx):
            "roofline": roofline(alg, clk.avg(), "k_groupby<file_id>",
                                 "25 B/event (inode 8, dev 4, pid 4, tid 4, op 1, count 4) + 60 B/group", "c5",
                                 {"events": n, "keys": G})}
+    if a.check and world == 1:
+        O = ctx["O"]
+        h = O.gen_file(0xC5, 0, G, cdf_h, 0, n)
+        keys = O.pad_keys(h, ("inode", "dev", "pid", "tid"))
+        out["check"] = check_table(a, ctx, tab, st["cand"], keys, c5_oracle_aggs(h), None, 4, [(3, True)], K)
+        out["check"]["what"] = ("last timed interval's table vs oracle or_groupby_topk_mt on the same stream: "
+                                "group count, checksum of every (key, reads, rbytes, writes, wbytes, first), "
+                                "top-20 by [-wbytes] (first + 4 aggregates)")
+        del h, keys
+    elif a.check and rank == 0:
+        out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
+                                   "tests/test_gpu_dist.py"}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 10_000_000
@@ -585,13 +739,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     igx = importlib.import_module("inspektor-gadget_amd")
-    O = None
-    if rank == 0 and world == 1 and (a.cpu_sample or a.check):
-        from oracle import oracle as O   # CPU baselines / --check only (test infrastructure)
     if world > 1:
         transport = igx.dist.select_transport(a.transport)
-    ctx = {"torch": torch, "igx": igx, "E": igx.engine, "H": igx.columns, "A": igx._abi, "D": igx.dist,
-           "O": O, "rank": rank, "world": world, "dev": dev, "timer": Timer(torch, dist, world, dev)}
+    ctx = make_ctx(torch, dist, igx, rank, world, dev, a.check or (rank == 0 and world == 1 and a.cpu_sample))
 
     c2 = run_c2(a, ctx)
     configs = {}
@@ -600,6 +750,7 @@ def main():
         configs[name] = fn(a, ctx)
         torch.cuda.empty_cache()
 
+    failed = []
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -626,13 +777,32 @@ def main():
             "roofline": c2["roofline"],
             "cpu_baseline": c2.get("cpu_baseline"),
             "configs": configs,
+            "library": os.path.relpath(igx._abi.LIB_PATH, ROOT),
         }
         if "check" in c2:
             line["check"] = c2["check"]
+            line["check"]["configs"] = {k: v["check"].get("bit_exact", "skipped")
+                                        for k, v in configs.items() if "check" in v}
+            failed = [k for k, v in [("c2", c2)] + list(configs.items())
+                      if v.get("check", {}).get("bit_exact") is False]
+            line["check"]["all_bit_exact"] = not failed
         print(json.dumps(line), flush=True)
     if world > 1:
         igx.dist.shutdown()
         dist.destroy_process_group()
+    if failed:
+        print(f"bench.py: results differ from the oracle in {failed}", file=sys.stderr, flush=True)
+        sys.exit(3)
+
+
+def make_ctx(torch, dist, igx, rank, world, dev, need_oracle):
+    """The per-process handles every run_cX takes (tests/test_gpu_fullsize.py builds the same
+    one to run the bench's exact steps)."""
+    O = None
+    if need_oracle:
+        from oracle import oracle as O   # CPU baselines and the post-run check only (test infrastructure)
+    return {"torch": torch, "dist": dist, "igx": igx, "E": igx.engine, "H": igx.columns, "A": igx._abi,
+            "D": igx.dist, "O": O, "rank": rank, "world": world, "dev": dev, "timer": Timer(torch, dist, world, dev)}
 
 
 if __name__ == "__main__":

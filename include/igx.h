@@ -434,15 +434,27 @@ int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32
  * with igx_dist_plan_* below, so either every rank proceeds or every rank returns the same
  * error (IGX_ENOSPC, or IGX_EINVAL when some rank's arguments are invalid).  With out == NULL
  * on every rank they are a size query: the counts are exchanged and returned, no rows move.
- * A failure inside the RCCL send/recv group (IGX_EIO) closes the group and marks the
- * communicator broken: every later call on it returns IGX_EIO. */
+ * Failure detection: the communicator is non-blocking and every wait inside these calls (a call
+ * still being issued, the stream draining after the metadata all-gather, igx_dist_wait) polls
+ * ncclCommGetAsyncError under a deadline (IGX_DIST_TIMEOUT_MS, default 120000, or
+ * igx_dist_set_timeout).  An RCCL error, an asynchronous error or a missed deadline -- a peer
+ * that died mid-collective -- returns IGX_EIO, aborts this rank's communicator (ncclCommAbort:
+ * its kernels waiting on the peer exit) and marks it broken: every later call returns IGX_EIO
+ * at once.  The reference drops a node that stops answering after its TTL instead of waiting on
+ * it (pkg/snapshotcombiner/snapshotcombiner.go:91-100). */
 #define IGX_DIST_ID_BYTES 128
 typedef struct igx_dist igx_dist;
 int igx_dist_get_unique_id(uint8_t *out_id);
 int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int rank, igx_dist **out);
 int igx_dist_destroy(igx_dist *d);
 int igx_dist_rank(igx_dist *d, int *rank, int *nranks);
-int igx_dist_barrier(igx_dist *d);   /* synchronises */
+int igx_dist_barrier(igx_dist *d);   /* synchronises (bounded) */
+/* The deadline of every wait on this communicator, in ms (> 0). */
+int igx_dist_set_timeout(igx_dist *d, int timeout_ms);
+/* Bounded hipStreamSynchronize of the context's stream for a caller that must wait on an
+ * asynchronous collective (igx_dist_allreduce_u32, the row exchanges' data phase): IGX_EIO, and
+ * the communicator aborted, on an RCCL error or when the deadline passes. */
+int igx_dist_wait(igx_dist *d);
 /* Marks the communicator unusable, as a failed group does: every later call returns IGX_EIO
  * without entering a collective.  For a caller that learned of a peer's failure out of band
  * (e.g. a node's gRPC stream ended, grpc-runtime.go:221-237). */
@@ -523,6 +535,14 @@ int igx_ingest_open_events(igx_ctx *ctx, const uint8_t *samples, uint64_t n, uin
 int igx_ingest_aos(igx_ctx *ctx, const void *records, uint64_t nrec, uint32_t rec_bytes,
                    const uint32_t *field_off, const uint32_t *field_width, uint32_t nfields,
                    void *const *out_cols);
+
+/* ---- test hooks (k_debug.hip; not part of the aggregation path) ----
+ * igx_debug_hold_stream: one wave on the context's stream that waits on a host-mapped flag
+ * (at most ~max_ms), so a test can make a collective queued behind it miss igx_dist's deadline
+ * the way a dead peer would.  igx_debug_release sets the flag, waits for the stream, frees the
+ * token; *how = 1 if the wave saw the release, 2 if its own budget ran out. */
+int igx_debug_hold_stream(igx_ctx *ctx, uint32_t max_ms, void **token);
+int igx_debug_release(igx_ctx *ctx, void *token, uint32_t *how);
 
 /* ---- synthetic event generators (device; bit-identical with oracle/igx_oracle.c) ---- */
 int igx_gen_tcp(igx_ctx *ctx, uint64_t seed, uint64_t rank, uint64_t G, uint64_t permA,

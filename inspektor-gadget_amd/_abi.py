@@ -8,6 +8,11 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IGX_LIB") or os.path.join(HERE, "libigx.so")   # IGX_LIB: A/B builds
+if os.environ.get("IGX_LIB"):
+    # an experimental build replaces the in-tree one for the whole process: say so, and
+    # bench.py records the path in its JSON line (`library`)
+    import sys as _sys
+    print(f"inspektor-gadget_amd: IGX_LIB={LIB_PATH}", file=_sys.stderr, flush=True)
 
 IGX_OK = 0
 IGX_ENOENT = -2
@@ -157,6 +162,8 @@ SIGNATURES = [
     ("igx_dist_rank", _I, [_VP, C.POINTER(_I), C.POINTER(_I)]),
     ("igx_dist_barrier", _I, [_VP]),
     ("igx_dist_mark_broken", _I, [_VP]),
+    ("igx_dist_set_timeout", _I, [_VP, _I]),
+    ("igx_dist_wait", _I, [_VP]),
     ("igx_dist_allreduce_u32", _I, [_VP, _VP, _U64]),
     ("igx_dist_allgather_rows", _I, [_VP, _VP, _U64, _U32, _VP, _U64, C.POINTER(_U64)]),
     ("igx_dist_alltoallv_rows", _I, [_VP, _VP, C.POINTER(_U64), _U32, _VP, _U64, C.POINTER(_U64)]),
@@ -166,6 +173,8 @@ SIGNATURES = [
     ("igx_ingest_open_events", _I, [_VP, _VP, _U64, _U32, C.c_int64, C.POINTER(OpenCols)]),
     ("igx_ingest_aos", _I, [_VP, _VP, _U64, _U32, C.POINTER(_U32), C.POINTER(_U32), _U32,
                             C.POINTER(_VP)]),
+    ("igx_debug_hold_stream", _I, [_VP, _U32, C.POINTER(_VP)]),
+    ("igx_debug_release", _I, [_VP, _VP, C.POINTER(_U32)]),
     ("igx_gen_tcp", _I, [_VP, _U64, _U64, _U64, _U64, _U64, _VP, _U64, _U64] + [_VP] * 10),
     ("igx_gen_open", _I, [_VP, _U64, _VP, _U64, _U64] + [_VP] * 8),
     ("igx_gen_bio", _I, [_VP, _U64, _VP, _U64, _U64, _U64, _VP, _VP, _VP]),

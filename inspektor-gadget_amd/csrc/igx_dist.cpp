@@ -15,7 +15,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "igx_internal.h"
@@ -24,7 +29,9 @@ struct igx_dist {
     igx_ctx *ctx = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
-    bool broken = false;          // an RCCL call failed inside a group: the communicator is unusable
+    int timeout_ms = 0;           // bound on every wait (IGX_DIST_TIMEOUT_MS / igx_dist_set_timeout)
+    bool broken = false;          // a call failed or timed out: the communicator is aborted and unusable
+    bool stuck = false;           // the stream did not drain before a deadline: keep its buffers alive
     uint64_t *d_meta = nullptr;   // device: own meta, then all ranks' meta (sized at init)
     uint64_t *h_meta = nullptr;   // pinned host copy of all ranks' meta
     size_t meta_words = 0;        // per-rank words the buffers hold
@@ -33,37 +40,114 @@ struct igx_dist {
     uint64_t *d_cnt = nullptr;    // exchange_groups: rows per owner
 };
 
-// a group's end: when it fails, the peers' matching sends / receives may never complete, so
-// the communicator is marked unusable (later calls fail with IGX_EIO before any collective)
-#define IGX_NCCL_END(d)                                                                     \
-    do {                                                                                    \
-        ncclResult_t r_ = ncclGroupEnd();                                                   \
-        if (r_ != ncclSuccess) {                                                            \
-            (d)->broken = true;                                                             \
-            return igx_fail((d)->ctx, IGX_EIO, "ncclGroupEnd: %s", ncclGetErrorString(r_)); \
-        }                                                                                   \
+// ---- failure detection ----------------------------------------------------------------
+// The communicator is non-blocking (ncclConfig_t.blocking = 0): no RCCL call waits on a peer
+// inside the library.  Every wait -- a call still being issued (ncclInProgress), or the
+// stream draining after a collective -- polls ncclCommGetAsyncError under a deadline.  A peer
+// that died mid-collective therefore surfaces as IGX_EIO on every survivor within the
+// deadline instead of a hang; the survivors' communicators are aborted (ncclCommAbort makes
+// their RCCL kernels that wait on the dead peer exit) and marked broken, so every later call
+// fails at once.  The reference's counterpart drops a silent node after its TTL instead of
+// waiting on it (pkg/snapshotcombiner/snapshotcombiner.go:91-100; grpc-runtime.go:312-315
+// ends a node's stream on error).
+static constexpr int DEFAULT_TIMEOUT_MS = 120000;
+
+static int env_timeout_ms() {
+    const char *e = std::getenv("IGX_DIST_TIMEOUT_MS");
+    if (e && *e) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0 && v < (1L << 30)) return (int)v;
+    }
+    return DEFAULT_TIMEOUT_MS;
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static void dist_abort(igx_dist *d) {
+    d->broken = true;
+    if (d->comm) {
+        (void)ncclCommAbort(d->comm);
+        d->comm = nullptr;
+    }
+}
+
+// marks the communicator broken (aborting it) and fails the call with IGX_EIO
+static int dist_fail(igx_dist *d, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static int dist_fail(igx_dist *d, const char *fmt, ...) {
+    char buf[768];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    dist_abort(d);
+    return igx_fail(d->ctx, IGX_EIO, "%s (communicator aborted)", buf);
+}
+
+// an RCCL call's result on the non-blocking communicator: ncclInProgress is polled until the
+// call is issued, under the deadline; any error aborts the communicator
+static int nccl_settle(igx_dist *d, ncclResult_t r, const char *what) {
+    const double t0 = now_ms();
+    while (r == ncclInProgress) {
+        if (now_ms() - t0 > d->timeout_ms) return dist_fail(d, "%s: not issued within %d ms", what, d->timeout_ms);
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (ncclCommGetAsyncError(d->comm, &r) != ncclSuccess) r = ncclInternalError;
+    }
+    if (r != ncclSuccess) return dist_fail(d, "%s: %s", what, ncclGetErrorString(r));
+    return IGX_OK;
+}
+
+// waits for the context's stream (collectives included) under the deadline, watching the
+// communicator's asynchronous error: the bounded replacement of hipStreamSynchronize
+static int dist_sync(igx_dist *d, const char *what) {
+    igx_ctx *ctx = d->ctx;
+    const double t0 = now_ms();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(ctx->stream);
+        if (e == hipSuccess) return IGX_OK;
+        if (e != hipErrorNotReady) {
+            d->stuck = true;
+            return dist_fail(d, "%s: %s", what, hipGetErrorString(e));
+        }
+        ncclResult_t a = ncclSuccess;
+        if (d->comm && ncclCommGetAsyncError(d->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
+            d->stuck = true;
+            return dist_fail(d, "%s: asynchronous error %s", what, ncclGetErrorString(a));
+        }
+        if (now_ms() - t0 > d->timeout_ms) {
+            d->stuck = true;
+            return dist_fail(d, "%s: timed out after %d ms", what, d->timeout_ms);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+#define IGX_DIST_LIVE(d)                                                                  \
+    do {                                                                                  \
+        if ((d)->broken || !(d)->comm)                                                    \
+            return igx_fail((d)->ctx, IGX_EIO, "dist: communicator broken by an earlier failure"); \
     } while (0)
+// an RCCL call outside a group
+#define IGX_NCCL(d, expr)                                      \
+    do {                                                       \
+        int rc_ = nccl_settle((d), (expr), #expr);             \
+        if (rc_) return rc_;                                   \
+    } while (0)
+// inside ncclGroupStart/End: a failure aborts the communicator (which ends the group) and
+// marks it broken -- the peers' matching sends / receives may never complete
+#define IGX_NCCL_G(d, expr)                                                                  \
+    do {                                                                                     \
+        ncclResult_t r_ = (expr);                                                            \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) {                                     \
+            (void)ncclGroupEnd();   /* the group depth is per thread: close it first */     \
+            return dist_fail((d), "%s: %s", #expr, ncclGetErrorString(r_));                 \
+        }                                                                                    \
+    } while (0)
+#define IGX_NCCL_END(d) IGX_NCCL(d, ncclGroupEnd())
 
 // the widest per-rank meta row any call gathers: alltoallv's send counts, capacity, flags
 static constexpr size_t META_WORDS = IGX_DIST_MAX_RANKS + 2;
-
-#define IGX_NCCL(d, expr)                                                                   \
-    do {                                                                                    \
-        ncclResult_t r_ = (expr);                                                           \
-        if (r_ != ncclSuccess)                                                              \
-            return igx_fail((d)->ctx, IGX_EIO, "%s: %s", #expr, ncclGetErrorString(r_));    \
-    } while (0)
-// inside ncclGroupStart/End: close the group before failing, and mark the communicator broken
-// (the peers' matching sends / receives may never complete, so it must not be reused)
-#define IGX_NCCL_G(d, expr)                                                                 \
-    do {                                                                                    \
-        ncclResult_t r_ = (expr);                                                           \
-        if (r_ != ncclSuccess) {                                                            \
-            (void)ncclGroupEnd();                                                           \
-            (d)->broken = true;                                                             \
-            return igx_fail((d)->ctx, IGX_EIO, "%s: %s", #expr, ncclGetErrorString(r_));    \
-        }                                                                                   \
-    } while (0)
 
 // ---- planning (host only; tests/test_dist_plan.py checks it against gloo's all-to-all) ----
 static void plan_reset(igx_dist_plan *p) {
@@ -141,54 +225,87 @@ extern "C" int igx_dist_get_unique_id(uint8_t *out_id) {
 extern "C" int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int rank, igx_dist **out) {
     if (!ctx || !id || !out) return IGX_EINVAL;
     *out = nullptr;
-    if (nranks < 1 || rank < 0 || rank >= nranks)
+    if (nranks < 1 || rank < 0 || rank >= nranks)   // every rank gets the same nranks: all fail alike
         return igx_fail(ctx, IGX_EINVAL, "dist_init: rank %d of %d", rank, nranks);
-    IGX_HIP(ctx, hipSetDevice(ctx->device));
-    ncclUniqueId uid;
-    std::memcpy(uid.internal, id, IGX_DIST_ID_BYTES);
     if (nranks > IGX_DIST_MAX_RANKS)
         return igx_fail(ctx, IGX_ENOTSUP, "dist_init: more than %d ranks", IGX_DIST_MAX_RANKS);
     auto *d = new igx_dist();
     d->ctx = ctx;
     d->rank = rank;
     d->nranks = nranks;
-    // the metadata buffers are sized once here, so no collective ever allocates (an
-    // allocation failure on one rank would leave the others waiting in the all-gather)
+    d->timeout_ms = env_timeout_ms();
+    // A local failure (device, allocation) must not skip the communicator's creation: the
+    // peers' ncclCommInitRank waits for every rank.  Such a rank joins, then aborts its side.
+    // The metadata buffers are sized once here, so no collective ever allocates.
+    const hipError_t dev_e = hipSetDevice(ctx->device);
     const bool mem_ok =
-        hipMalloc(&d->d_meta, META_WORDS * (nranks + 1) * 8) == hipSuccess &&
+        dev_e == hipSuccess && hipMalloc(&d->d_meta, META_WORDS * (nranks + 1) * 8) == hipSuccess &&
         hipHostMalloc(reinterpret_cast<void **>(&d->h_meta), META_WORDS * (nranks + 1) * 8, hipHostMallocDefault) ==
             hipSuccess;
     d->meta_words = META_WORDS;
-    // every rank joins the communicator's creation, even one whose allocation failed: the
-    // peers' ncclCommInitRank waits for all ranks; a failed rank then aborts its side
-    const ncclResult_t r = ncclCommInitRank(&d->comm, nranks, uid, rank);
-    if (r != ncclSuccess || !mem_ok) {
-        if (r == ncclSuccess) (void)ncclCommAbort(d->comm);
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, IGX_DIST_ID_BYTES);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;   // every wait is ours, under the deadline (nccl_settle / dist_sync)
+    int rc = nccl_settle(d, ncclCommInitRankConfig(&d->comm, nranks, uid, rank, &cfg), "ncclCommInitRankConfig");
+    if (!rc && !mem_ok) dist_abort(d);
+    if (rc || !mem_ok) {
         (void)hipFree(d->d_meta);
         (void)hipHostFree(d->h_meta);
         delete d;
-        if (!mem_ok) return igx_fail(ctx, IGX_ENOMEM, "dist_init: metadata buffers");
-        return igx_fail(ctx, IGX_EIO, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+        if (rc) return rc;   // ctx->err names the RCCL failure or the timeout
+        if (dev_e != hipSuccess) return igx_fail(ctx, IGX_EIO, "dist_init: hipSetDevice(%d): %s", ctx->device,
+                                                 hipGetErrorString(dev_e));
+        return igx_fail(ctx, IGX_ENOMEM, "dist_init: metadata buffers");
     }
     *out = d;
     return IGX_OK;
 }
 
+extern "C" int igx_dist_set_timeout(igx_dist *d, int timeout_ms) {
+    if (!d || timeout_ms <= 0) return IGX_EINVAL;
+    d->timeout_ms = timeout_ms;
+    return IGX_OK;
+}
+
+extern "C" int igx_dist_wait(igx_dist *d) {
+    if (!d) return IGX_EINVAL;
+    IGX_DIST_LIVE(d);
+    return dist_sync(d, "dist_wait");
+}
+
 extern "C" int igx_dist_destroy(igx_dist *d) {
     if (!d) return IGX_OK;
-    (void)hipStreamSynchronize(d->ctx->stream);
-    if (d->comm) (void)ncclCommDestroy(d->comm);
-    (void)hipFree(d->d_meta);
-    (void)hipHostFree(d->h_meta);
-    (void)hipFree(d->part);
-    (void)hipFree(d->d_cnt);
+    // a stream that cannot drain (a peer died, the communicator was aborted, yet some kernel
+    // still runs) keeps the buffers: freeing memory a running kernel uses is worse than a leak
+    bool drained = !d->stuck;
+    if (drained && d->comm) drained = dist_sync(d, "dist_destroy") == IGX_OK;
+    else if (drained) {
+        const double t0 = now_ms();
+        hipError_t e;
+        while ((e = hipStreamQuery(d->ctx->stream)) == hipErrorNotReady && now_ms() - t0 < d->timeout_ms)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        drained = e == hipSuccess;
+    }
+    if (d->comm) {
+        if (nccl_settle(d, ncclCommFinalize(d->comm), "ncclCommFinalize") == IGX_OK) {
+            (void)ncclCommDestroy(d->comm);
+            d->comm = nullptr;
+        }
+    }
+    if (drained) {
+        (void)hipFree(d->d_meta);
+        (void)hipHostFree(d->h_meta);
+        (void)hipFree(d->part);
+        (void)hipFree(d->d_cnt);
+    }
     delete d;
     return IGX_OK;
 }
 
 extern "C" int igx_dist_mark_broken(igx_dist *d) {
     if (!d) return IGX_EINVAL;
-    d->broken = true;
+    dist_abort(d);   // this rank's RCCL kernels that wait on the failed peer exit too
     return IGX_OK;
 }
 
@@ -203,7 +320,7 @@ extern "C" int igx_dist_rank(igx_dist *d, int *rank, int *nranks) {
 // d->h_meta[rank * words + i].  Synchronises the stream.  Allocates nothing.
 static int gather_meta(igx_dist *d, const uint64_t *mine, size_t words) {
     igx_ctx *ctx = d->ctx;
-    if (d->broken) return igx_fail(ctx, IGX_EIO, "dist: communicator broken by an earlier failure");
+    IGX_DIST_LIVE(d);
     if (words > d->meta_words) return igx_fail(ctx, IGX_EINVAL, "dist: %zu meta words", words);
     uint64_t *h_send = d->h_meta + words * d->nranks;   // the spare row of the pinned buffer
     std::memcpy(h_send, mine, words * 8);
@@ -211,8 +328,7 @@ static int gather_meta(igx_dist *d, const uint64_t *mine, size_t words) {
     IGX_NCCL(d, ncclAllGather(d->d_meta, d->d_meta + words, words, ncclUint64, d->comm, ctx->stream));
     IGX_HIP(ctx, hipMemcpyAsync(d->h_meta, d->d_meta + words, words * d->nranks * 8, hipMemcpyDeviceToHost,
                                 ctx->stream));
-    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return IGX_OK;
+    return dist_sync(d, "dist: metadata all-gather");
 }
 
 static int plan_fail(igx_dist *d, const igx_dist_plan &p, const char *what) {
@@ -224,24 +340,20 @@ static int plan_fail(igx_dist *d, const igx_dist_plan &p, const char *what) {
 
 extern "C" int igx_dist_allreduce_u32(igx_dist *d, uint32_t *buf, uint64_t n) {
     if (!d) return IGX_EINVAL;
-    if (d->broken) return igx_fail(d->ctx, IGX_EIO, "dist: communicator broken by an earlier failure");
+    IGX_DIST_LIVE(d);
     if (n == 0) return IGX_OK;
     if (!buf) {
         // the peers are already in (or will enter) the all-reduce of n words: take part with
         // zeros so they complete, then fail this rank's call
         void *z = nullptr;
         if (igx_scratch(d->ctx, n * 4, &z) || hipMemsetAsync(z, 0, n * 4, d->ctx->stream) != hipSuccess ||
-            ncclAllReduce(z, z, n, ncclUint32, ncclSum, d->comm, d->ctx->stream) != ncclSuccess)
-            d->broken = true;
+            nccl_settle(d, ncclAllReduce(z, z, n, ncclUint32, ncclSum, d->comm, d->ctx->stream), "ncclAllReduce"))
+            dist_abort(d);
         return igx_fail(d->ctx, IGX_EINVAL, "dist_allreduce: null buffer");
     }
     // u32 addition mod 2^32 is exact and order-independent: the merged histogram equals the
     // histogram of the union of every rank's events
-    const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, d->comm, d->ctx->stream);
-    if (r != ncclSuccess) {
-        d->broken = true;
-        return igx_fail(d->ctx, IGX_EIO, "ncclAllReduce: %s", ncclGetErrorString(r));
-    }
+    IGX_NCCL(d, ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, d->comm, d->ctx->stream));
     return IGX_OK;
 }
 
@@ -329,7 +441,7 @@ extern "C" int igx_dist_exchange_groups(igx_dist *d, const void *rows, uint64_t 
     int lerr = IGX_OK;
     const size_t need = (size_t)nrows * row_bytes;
     if (need > d->part_bytes) {
-        (void)hipStreamSynchronize(ctx->stream);
+        if (dist_sync(d, "dist_exchange_groups")) return IGX_EIO;   // the buffer may still be read
         (void)hipFree(d->part);
         d->part = nullptr;
         d->part_bytes = 0;
@@ -343,9 +455,9 @@ extern "C" int igx_dist_exchange_groups(igx_dist *d, const void *rows, uint64_t 
     if (!lerr && nrows) {
         lerr = igx_partition_rows(ctx, static_cast<const uint8_t *>(rows), nrows, row_bytes, key_bytes, (uint32_t)nr,
                                   d->part, d->d_cnt);
-        if (!lerr && (hipMemcpyAsync(cnt, d->d_cnt, nr * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-                      hipStreamSynchronize(ctx->stream) != hipSuccess))
+        if (!lerr && hipMemcpyAsync(cnt, d->d_cnt, nr * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
             lerr = IGX_EIO;
+        if (!lerr && dist_sync(d, "dist_exchange_groups: partition counts")) return IGX_EIO;   // aborted: no peer waits
     }
     uint64_t rc_[IGX_DIST_MAX_RANKS] = {};
     if (lerr) {

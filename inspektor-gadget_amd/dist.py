@@ -99,28 +99,43 @@ class IgxComm:
 
     name = "igx"
 
-    def __init__(self, d):
+    def __init__(self, d, timeout_ms=None):
         torch = torch_mod()
-        self.ctx = context()
-        L = self.ctx.L
         from . import _abi
         rank, ws = d.get_rank(), d.get_world_size()
+        self.h, self.ws = None, ws
         uid = (C.c_uint8 * _abi.DIST_ID_BYTES)()
-        ok = 1
-        if rank == 0:
-            ok = int(L.igx_dist_get_unique_id(uid) == 0)
-        # every rank joins the broadcast, a failed id included (its last byte says so), so no
-        # rank is left waiting in it while rank 0 moves on to the next collective
-        t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=torch.device("cuda", self.ctx.device))
+        ok, err = 1, None
+        try:
+            self.ctx = context()
+            if rank == 0:
+                ok = int(self.ctx.L.igx_dist_get_unique_id(uid) == 0)
+            dev = torch.device("cuda", self.ctx.device)
+        except Exception as e:   # noqa: BLE001 -- still join the broadcast below, flagged
+            ok, err, dev = 0, e, torch.device("cuda", torch.cuda.current_device())
+        # every rank joins the broadcast whatever happened above (the last byte carries rank
+        # 0's status), so no rank is left waiting in it while the others move on
+        t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=dev)
         d.broadcast(t, 0)
         v = t.cpu().tolist()
+        if err is not None:
+            # this rank cannot open the transport; its peers, already past the broadcast, fail
+            # igx_dist_init within IGX_DIST_TIMEOUT_MS, and select_transport's all-reduce then
+            # moves every rank to the fallback
+            raise RuntimeError(f"IgxComm on rank {rank}: {err}")
         if not v[-1]:
             raise RuntimeError("igx_dist_get_unique_id failed on rank 0")
         uid = (C.c_uint8 * _abi.DIST_ID_BYTES)(*v[:-1])
         h = C.c_void_p()
-        self.ctx.check(L.igx_dist_init(self.ctx.h, uid, ws, rank, C.byref(h)))
+        self.ctx.check(self.ctx.L.igx_dist_init(self.ctx.h, uid, ws, rank, C.byref(h)))
         self.h = h
-        self.ws = ws
+        if timeout_ms is not None:
+            self.ctx.check(self.ctx.L.igx_dist_set_timeout(self.h, int(timeout_ms)))
+
+    def wait(self):
+        """igx_dist_wait: the stream drained, bounded by the communicator's deadline (EIO and
+        an aborted communicator when a peer stops answering)."""
+        self.ctx.check(self.ctx.L.igx_dist_wait(self.h))
 
     def _bind(self):
         self.ctx.bind_stream()
@@ -129,6 +144,7 @@ class IgxComm:
     def allreduce_u32(self, hist):
         L = self._bind()
         self.ctx.check(L.igx_dist_allreduce_u32(self.h, ptr(hist), hist.numel()))
+        self.wait()
         return hist
 
     def allgather_rows(self, rows):
@@ -141,6 +157,7 @@ class IgxComm:
         tot = sum(counts)
         out = torch.empty((max(1, tot), rb), dtype=rows.dtype, device=rows.device)
         self.ctx.check(L.igx_dist_allgather_rows(self.h, ptr(rows), n, rb, ptr(out), tot, counts))
+        self.wait()
         return out[:tot]
 
     def alltoallv_rows(self, rows, counts):
@@ -154,6 +171,7 @@ class IgxComm:
         tot = sum(rc)
         out = torch.empty((max(1, tot), rb), dtype=rows.dtype, device=rows.device)
         self.ctx.check(L.igx_dist_alltoallv_rows(self.h, ptr(rows), sc, rb, ptr(out), tot, rc))
+        self.wait()
         return out[:tot]
 
     def barrier(self):

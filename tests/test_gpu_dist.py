@@ -99,6 +99,63 @@ def test_igx_dist_rccl_single_rank(igx, torch, oracle):
         ctx.check(L.igx_dist_destroy(h))
 
 
+DEADLINE_CHILD = r'''
+import ctypes as C, importlib, sys, time
+sys.path.insert(0, ROOT)
+import torch
+igx = importlib.import_module("inspektor-gadget_amd")
+A = igx._abi
+torch.cuda.set_device(0)
+ctx = igx.runtime.context()
+L = ctx.L
+ctx.bind_stream()
+uid = (C.c_uint8 * A.DIST_ID_BYTES)()
+assert L.igx_dist_get_unique_id(uid) == 0
+h = C.c_void_p()
+ctx.check(L.igx_dist_init(ctx.h, uid, 1, 0, C.byref(h)))
+ctx.check(L.igx_dist_barrier(h))                         # healthy first
+ctx.check(L.igx_dist_set_timeout(h, 1000))
+tok = C.c_void_p()
+ctx.check(L.igx_debug_hold_stream(ctx.h, 8000, C.byref(tok)))   # the stream stops here (<= ~8 s)
+t0 = time.time()
+rc = L.igx_dist_barrier(h)                               # its all-gather queues behind the held wave
+dt = time.time() - t0
+msg = L.igx_last_error(ctx.h).decode()
+assert rc == A.IGX_EIO, (rc, msg)
+assert "timed out after 1000 ms" in msg, msg
+assert 0.9 < dt < 30.0, dt
+# broken: every later call fails at once, without entering a collective
+t1 = time.time()
+assert L.igx_dist_barrier(h) == A.IGX_EIO
+assert L.igx_dist_wait(h) == A.IGX_EIO
+assert L.igx_dist_allreduce_u32(h, None, 0) == A.IGX_EIO
+assert time.time() - t1 < 0.5
+how = C.c_uint32()
+ctx.check(L.igx_debug_release(ctx.h, tok, C.byref(how)))   # release the wave, stream drains
+assert how.value == 1, how.value
+ctx.check(L.igx_dist_destroy(h))
+# a fresh communicator on the same context works again
+h2 = C.c_void_p()
+assert L.igx_dist_get_unique_id(uid) == 0
+ctx.check(L.igx_dist_init(ctx.h, uid, 1, 0, C.byref(h2)))
+ctx.check(L.igx_dist_barrier(h2))
+ctx.check(L.igx_dist_wait(h2))
+ctx.check(L.igx_dist_destroy(h2))
+print(f"DEADLINE_OK {dt:.2f}s")
+'''
+
+
+def test_igx_dist_deadline_aborts_instead_of_hanging():
+    """Failure detection (SURVEY §5: ncclCommGetAsyncError + timeout; the reference drops a
+    silent node after its TTL, snapshotcombiner.go:91-100): a collective that cannot complete --
+    here a one-rank barrier queued behind a wave held on a host-mapped flag, as a dead peer
+    would hold it -- returns IGX_EIO within the communicator's deadline with the communicator
+    aborted and broken, instead of hanging in hipStreamSynchronize.  In a child process."""
+    code = f"ROOT = {ROOT!r}\n" + DEADLINE_CHILD
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and "DEADLINE_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_igx_comm_transport_single_rank():
     """dist.IgxComm (the bench's N > 1 transport) built through a real one-rank "nccl" group:
     rank 0's unique id + status byte broadcast, igx_dist_init, an all-reduce, close -- in a

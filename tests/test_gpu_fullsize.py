@@ -146,3 +146,34 @@ def test_c5_full_size_table_and_topk(oracle, igx, torch):
         assert np.array_equal(t64(52), first), i
         for a in range(4):
             assert np.array_equal(t64(20 + 8 * a), aggs[:, a]), (i, a)
+
+
+# ------------------------------------------------------------------------------------
+# the bench's own measured step, verbatim: bench.run_c2 / run_c5 at their default sizes with
+# back-to-back asynchronous intervals (finalize(sync=False), the device-count top-K, no host
+# sync inside a step; AUTO's loader / form switching between intervals), then bench's
+# post-run check of the LAST interval against the oracle
+# ------------------------------------------------------------------------------------
+def _bench_ctx(igx, torch):
+    import torch.distributed as dist
+    bench = importlib.import_module("bench")
+    return bench, bench.make_ctx(torch, dist, igx, 0, 1, torch.device("cuda", 0), True)
+
+
+def test_bench_c2_async_intervals_match_oracle(igx, torch):
+    bench, ctx = _bench_ctx(igx, torch)
+    a = bench.parse(["--steps", "5", "--warmup", "1", "--cpu-sample", "0"])
+    out = bench.run_c2(a, ctx)
+    ck = out["check"]
+    assert ck["groups_equal"] and ck["table_checksum_equal"] and ck["topk_equal"], ck
+    assert ck["bit_exact"] is True
+
+
+def test_bench_c5_async_intervals_match_oracle(igx, torch):
+    bench, ctx = _bench_ctx(igx, torch)
+    a = bench.parse(["--config-steps", "5", "--cpu-sample", "0"])
+    out = bench.run_c5(a, ctx)
+    ck = out["check"]
+    assert ck["groups_equal"] and ck["table_checksum_equal"] and ck["topk_equal"], ck
+    assert ck["bit_exact"] is True
+    torch.cuda.empty_cache()

@@ -7,11 +7,11 @@ export TMPDIR=/tmp
 R=${1:-r03}
 O=gpurun_out/$R
 rm -rf $O; mkdir -p $O
-B="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --config-steps 3"
+B="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --config-steps 3 --no-check"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/trace.log 2>&1 || { echo "trace failed rc=$?"; tail $O/trace.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o p -- $B > $O/fetch.log 2>&1 || { echo "fetch failed rc=$?"; tail $O/fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o p -- $B > $O/write.log 2>&1 || { echo "write failed rc=$?"; tail $O/write.log; exit 1; }
-C2="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --configs="
+C2="python3 bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-check --configs="
 timeout -k 10 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/tcc1 -o p -- $C2 > $O/tcc1.log 2>&1 || { echo "tcc1 failed rc=$?"; tail $O/tcc1.log; exit 1; }
 timeout -k 10 200 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace --output-format csv -d $O/tcc2 -o p -- $C2 > $O/tcc2.log 2>&1 || { echo "tcc2 failed rc=$?"; tail $O/tcc2.log; exit 1; }
 timeout -k 10 200 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_64B_sum --kernel-trace --output-format csv -d $O/tcc3 -o p -- $C2 > $O/tcc3.log 2>&1 || echo "tcc3 failed rc=$? (optional)"
