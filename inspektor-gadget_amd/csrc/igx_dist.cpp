@@ -15,11 +15,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -31,13 +33,14 @@ struct igx_dist {
     int rank = 0, nranks = 1;
     int timeout_ms = 0;           // bound on every wait (IGX_DIST_TIMEOUT_MS / igx_dist_set_timeout)
     bool broken = false;          // a call failed or timed out: the communicator is aborted and unusable
-    bool stuck = false;           // the stream did not drain before a deadline: keep its buffers alive
     uint64_t *d_meta = nullptr;   // device: own meta, then all ranks' meta (sized at init)
     uint64_t *h_meta = nullptr;   // pinned host copy of all ranks' meta
     size_t meta_words = 0;        // per-rank words the buffers hold
     uint8_t *part = nullptr;      // exchange_groups: rows grouped by owner
     size_t part_bytes = 0;
     uint64_t *d_cnt = nullptr;    // exchange_groups: rows per owner
+    std::thread *aborter = nullptr;                  // runs ncclCommAbort (see dist_abort)
+    std::shared_ptr<std::atomic<int>> abort_done;    // set by the aborter when ncclCommAbort returned
 };
 
 // ---- failure detection ----------------------------------------------------------------
@@ -65,12 +68,38 @@ static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// ncclCommAbort runs on a helper thread: it returns once the communicator's own work has left
+// the GPU, and RCCL orders that work after whatever was queued before it on the caller's stream.
+// A collective waiting on a dead peer exits at once on the abort; work queued ahead of it in
+// the stream (another library's kernel, a stalled copy) may take longer, and this rank's call
+// must still fail within the deadline.  igx_dist_destroy reaps the thread.
 static void dist_abort(igx_dist *d) {
     d->broken = true;
-    if (d->comm) {
-        (void)ncclCommAbort(d->comm);
+    if (d->comm && !d->aborter) {
+        ncclComm_t c = d->comm;
         d->comm = nullptr;
+        auto done = std::make_shared<std::atomic<int>>(0);
+        d->abort_done = done;
+        d->aborter = new std::thread([c, done] {
+            (void)ncclCommAbort(c);
+            done->store(1, std::memory_order_release);
+        });
     }
+}
+
+// waits up to wait_ms for the aborter; true when it finished (joined), false when it is still
+// blocked (detached: it owns only the communicator handle and its own flag)
+static bool dist_reap(igx_dist *d, int wait_ms) {
+    if (!d->aborter) return true;
+    const double t0 = now_ms();
+    while (!d->abort_done->load(std::memory_order_acquire) && now_ms() - t0 < wait_ms)
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    const bool done = d->abort_done->load(std::memory_order_acquire) != 0;
+    if (done) d->aborter->join();
+    else d->aborter->detach();
+    delete d->aborter;
+    d->aborter = nullptr;
+    return done;
 }
 
 // marks the communicator broken (aborting it) and fails the call with IGX_EIO
@@ -107,16 +136,13 @@ static int dist_sync(igx_dist *d, const char *what) {
         const hipError_t e = hipStreamQuery(ctx->stream);
         if (e == hipSuccess) return IGX_OK;
         if (e != hipErrorNotReady) {
-            d->stuck = true;
             return dist_fail(d, "%s: %s", what, hipGetErrorString(e));
         }
         ncclResult_t a = ncclSuccess;
         if (d->comm && ncclCommGetAsyncError(d->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
-            d->stuck = true;
             return dist_fail(d, "%s: asynchronous error %s", what, ncclGetErrorString(a));
         }
         if (now_ms() - t0 > d->timeout_ms) {
-            d->stuck = true;
             return dist_fail(d, "%s: timed out after %d ms", what, d->timeout_ms);
         }
         std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -250,6 +276,7 @@ extern "C" int igx_dist_init(igx_ctx *ctx, const uint8_t *id, int nranks, int ra
     int rc = nccl_settle(d, ncclCommInitRankConfig(&d->comm, nranks, uid, rank, &cfg), "ncclCommInitRankConfig");
     if (!rc && !mem_ok) dist_abort(d);
     if (rc || !mem_ok) {
+        (void)dist_reap(d, d->timeout_ms);
         (void)hipFree(d->d_meta);
         (void)hipHostFree(d->h_meta);
         delete d;
@@ -276,11 +303,12 @@ extern "C" int igx_dist_wait(igx_dist *d) {
 
 extern "C" int igx_dist_destroy(igx_dist *d) {
     if (!d) return IGX_OK;
-    // a stream that cannot drain (a peer died, the communicator was aborted, yet some kernel
-    // still runs) keeps the buffers: freeing memory a running kernel uses is worse than a leak
-    bool drained = !d->stuck;
-    if (drained && d->comm) drained = dist_sync(d, "dist_destroy") == IGX_OK;
-    else if (drained) {
+    // a stream that cannot drain within the deadline (a peer died and some kernel still runs)
+    // keeps the buffers: freeing memory a running kernel uses is worse than a leak
+    bool drained;
+    if (d->comm) {
+        drained = dist_sync(d, "dist_destroy") == IGX_OK;   // aborts the communicator on failure
+    } else {
         const double t0 = now_ms();
         hipError_t e;
         while ((e = hipStreamQuery(d->ctx->stream)) == hipErrorNotReady && now_ms() - t0 < d->timeout_ms)
@@ -293,6 +321,7 @@ extern "C" int igx_dist_destroy(igx_dist *d) {
             d->comm = nullptr;
         }
     }
+    if (!dist_reap(d, d->timeout_ms)) drained = false;   // an abort still blocked: keep the buffers
     if (drained) {
         (void)hipFree(d->d_meta);
         (void)hipHostFree(d->h_meta);

@@ -102,6 +102,7 @@ def test_igx_dist_rccl_single_rank(igx, torch, oracle):
 DEADLINE_CHILD = r'''
 import ctypes as C, importlib, sys, time
 sys.path.insert(0, ROOT)
+print("start", flush=True)
 import torch
 igx = importlib.import_module("inspektor-gadget_amd")
 A = igx._abi
@@ -123,7 +124,8 @@ dt = time.time() - t0
 msg = L.igx_last_error(ctx.h).decode()
 assert rc == A.IGX_EIO, (rc, msg)
 assert "timed out after 1000 ms" in msg, msg
-assert 0.9 < dt < 30.0, dt
+print(f"barrier returned {rc} after {dt:.3f}s: {msg}", flush=True)
+assert 0.9 < dt < 5.0, dt                                # the deadline, not the held wave's ~8 s
 # broken: every later call fails at once, without entering a collective
 t1 = time.time()
 assert L.igx_dist_barrier(h) == A.IGX_EIO
@@ -131,7 +133,9 @@ assert L.igx_dist_wait(h) == A.IGX_EIO
 assert L.igx_dist_allreduce_u32(h, None, 0) == A.IGX_EIO
 assert time.time() - t1 < 0.5
 how = C.c_uint32()
+t2 = time.time()
 ctx.check(L.igx_debug_release(ctx.h, tok, C.byref(how)))   # release the wave, stream drains
+print(f"released after {time.time() - t0:.3f}s (wave ended {how.value}), drained in {time.time() - t2:.3f}s", flush=True)
 assert how.value == 1, how.value
 ctx.check(L.igx_dist_destroy(h))
 # a fresh communicator on the same context works again
@@ -153,6 +157,7 @@ def test_igx_dist_deadline_aborts_instead_of_hanging():
     aborted and broken, instead of hanging in hipStreamSynchronize.  In a child process."""
     code = f"ROOT = {ROOT!r}\n" + DEADLINE_CHILD
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=150)
+    print(r.stdout[-1500:])
     assert r.returncode == 0 and "DEADLINE_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 

@@ -3,7 +3,7 @@
 # counter group (rocprofv3 does not split passes).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/pmc5
+O=gpurun_out/pmc5${PMC_TAG}
 rm -rf $O; mkdir -p $O
 R="python3 tools/ablate_forms.py --configs c5,c2 --forms cached --reps 2"
 i=0
