@@ -597,6 +597,17 @@ def run_c4(a, ctx):
                                    "tests/test_gpu_dist.py"}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
+        # the reference's own path: GeneratePolicies builds a localPodKey / networkPeerKey string
+        # per event (label keys sorted, fmt.Sprintf) and dedups in string-keyed maps
+        # (advisor.go:130-159, 279-320) -- or_np_advise_strings, single-threaded like the Go code
+        SS = 4_000_000
+        hs = O.gen_np(*C4_GEN, 0, SS)
+        t0 = time.perf_counter()
+        gs = O.np_advise_strings(hs)
+        strings = time.perf_counter() - t0
+        assert gs == O.groupby(O.pad_keys(hs, names), [], valid=O.np_mark(hs))[0].shape[0]
+        del hs
+        # the same dedup over pre-packed integer keys (a lower bound of the CPU's cost)
         S = 20_000_000
         h = O.gen_np(*C4_GEN, 0, S)
         keys = O.pad_keys(h, names)
@@ -609,10 +620,17 @@ def run_c4(a, ctx):
         g2, _, _ = O.groupby_topk_mt(keys, [], valid=keep, threads=thr)
         multi = time.perf_counter() - t0
         assert g2 == len(k1)
-        out["cpu_baseline"] = cpu_entry(S, single, multi, thr, "events/s",
-                                        f"{S} events of the same stream (keys pre-packed, not timed): "
-                                        f"or_groupby_topk_mt distinct on {thr} threads; single_core = or_groupby "
-                                        "(GeneratePolicies' first-event-wins map, advisor.go:279-320)")
+        out["cpu_baseline"] = {
+            "value": SS / strings, "unit": "events/s", "cores": 1, "kind": "port", "seconds": strings,
+            "sample": f"{SS} events of the same stream through oracle/igx_oracle.c or_np_advise_strings: "
+                      "GeneratePolicies on the reference's string keys (localPodKey / networkPeerKey per "
+                      "event with sorted label keys, string-keyed first-event-wins maps, advisor.go:130-159, "
+                      "279-320), single-threaded like the Go code; same distinct count as the device",
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "prepacked": cpu_entry(S, single, multi, thr, "events/s",
+                                   f"{S} events, keys pre-packed as integers (not timed): or_groupby_topk_mt "
+                                   f"distinct on {thr} threads; single_core = or_groupby -- a lower bound of the "
+                                   "CPU path's cost, not the reference's shape")}
     tab.destroy()
     if own is not None:
         own.destroy()

@@ -208,7 +208,9 @@ int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, const char *con
  * Float keys compare as Go's `<` does: -0 == +0, -Inf < finite < +Inf; a NaN in a float key
  * of a non-nil row makes the comparison unordered (no strict weak order, so SliceStable's
  * output depends on its merge steps) and the call returns IGX_ENOTSUP.
- * out_perm (device u32, nrows).  Synchronises once (key range scan); otherwise async. */
+ * out_perm (device u32, nrows).  Asynchronous when no key is a float and the composed key is at
+ * most 8 words (the passes are planned on the device); otherwise synchronises once (key range
+ * and NaN scan). */
 int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                   const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm);
 
@@ -220,6 +222,17 @@ int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_
  * igx_sort_perm. */
 int igx_sort_perm_ex(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap, uint32_t *out_perm);
+
+/* igx_sort_perm_ex when the row count lives on the device: the slice is rows [0, *d_nrows) of
+ * the selection vector, nrows_max its upper bound (d_nrows: device u64, e.g. igx_filter's
+ * out_n) -- FilterEntries' count feeds SortEntries without a host round trip.  Composed keys
+ * of at most 8 words and no float key (a NaN would need the host's decision): otherwise
+ * IGX_EINVAL.  out_perm (device u32, nrows_max) holds the sorted rowmap values in its first
+ * *d_nrows entries.  Asynchronous: no host synchronisation at all (the passes are planned on
+ * the device).  igx_sort_perm / _ex plan the same way whenever their keys allow it. */
+int igx_sort_perm_dn(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows_max,
+                     const uint64_t *d_nrows, const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap,
+                     uint32_t *out_perm);
 
 /* First k rows of the igx_sort_perm order (SortStats + truncate to max-rows).
  * out_idx (device u32, k).  Asynchronous. */
@@ -315,8 +328,11 @@ typedef struct {
     uint32_t part_left;  /* AUTO: intervals still planned in the partitioned form */
     uint32_t exact_left; /* AUTO: intervals partitioned exactly after a region overflowed */
     uint32_t sm_probers; /* the cached form's probers: 1 state machine, 0 batch */
-    uint32_t pad;
+    uint32_t loaders;    /* the cached form's loader waves for the next update (8, or 7 after intervals
+                            that missed the LDS cache on > 39 % of their rows, until one falls below 37 %) */
     uint64_t rows;       /* rows fed to the interval so far */
+    uint32_t miss_permille;  /* LDS misses per 1000 rows of the last measured cached interval */
+    uint32_t pad;
 } igx_groupby_info_t;
 int igx_groupby_info(igx_table *t, igx_groupby_info_t *out);
 /* igx_groupby_finalize without its host synchronisation: the occupied-slot list is built on

@@ -54,8 +54,8 @@ class SortKey(C.Structure):
 
 class GroupbyInfo(C.Structure):
     _fields_ = [("form", C.c_uint32), ("region", C.c_uint32), ("part_left", C.c_uint32),
-                ("exact_left", C.c_uint32), ("sm_probers", C.c_uint32), ("pad", C.c_uint32),
-                ("rows", C.c_uint64)]
+                ("exact_left", C.c_uint32), ("sm_probers", C.c_uint32), ("loaders", C.c_uint32),
+                ("rows", C.c_uint64), ("miss_permille", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class Agg(C.Structure):
@@ -132,6 +132,7 @@ SIGNATURES = [
                               C.POINTER(SortKey), C.POINTER(_U32), C.POINTER(_U32)]),
     ("igx_sort_perm", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP]),
     ("igx_sort_perm_ex", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP, _VP]),
+    ("igx_sort_perm_dn", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _VP, _VP, _VP, _VP]),
     ("igx_topk", _I, [_VP, C.POINTER(SortKey), _U32, _U64, _VP, _U32, _VP]),
     ("igx_groupby_create", _I, [_VP, C.POINTER(_U32), _U32, C.POINTER(Agg), _U32, _U64,
                                 C.POINTER(_VP)]),

@@ -149,22 +149,44 @@ class EventBatch:
     sort.go:116-123), no entry copied.  Taking rows of a view composes the selection; a
     column of a view is gathered on first access (`batch[name]`, `data`, `valid`)."""
 
-    def __init__(self, cols: Columns, data: dict, valid=None, sel=None):
+    def __init__(self, cols: Columns, data: dict, valid=None, sel=None, sel_count=None):
         self.cols = cols
         self._base = {k.lower(): v for k, v in data.items()}
         self._base_valid = valid
         any_t = next(iter(self._base.values())) if self._base else valid
         self.base_n = 0 if any_t is None else int(any_t.shape[0])
         self.sel = sel
+        # a selection whose length is still on the device (u64 tensor): `sel` then has the
+        # capacity of its upper bound and `n` synchronises on first use (FilterEntries ->
+        # SortEntries runs without a host round trip: filter.FilterEntries, sort.Sort)
+        self.sel_count = sel_count if sel is not None else None
         self._mat = {}
         self._valid_mat = None
-        self.n = self.base_n if sel is None else int(sel.shape[0])
+        self._n = None if self.sel_count is not None else (self.base_n if sel is None else int(sel.shape[0]))
+
+    @property
+    def n(self):
+        if self._n is None:
+            k = int(self.sel_count.item())
+            self.sel = self.sel[:k]
+            self.sel_count = None
+            self._n = k
+        return self._n
+
+    @n.setter
+    def n(self, v):
+        self._n = v
+
+    def pending(self):
+        """(selection of capacity n_max, device count) while the length is on the device, else None."""
+        return (self.sel, self.sel_count) if self.sel_count is not None else None
 
     def __len__(self):
         return self.n
 
     def _gather(self, t):
         from . import engine                 # igx_take on the device
+        self.n                               # a device-side length is read (and sel trimmed) first
         return engine.take([t], self.sel, self.base_n)[0]
 
     def __getitem__(self, name):
@@ -208,6 +230,7 @@ class EventBatch:
     def base(self):
         """(base columns, base valid mask, selection or None) -- for passes that read a view
         through its selection vector instead of gathering it."""
+        self.n
         return self._base, self._base_valid, self.sel
 
     def device(self):

@@ -102,6 +102,7 @@ extern "C" int igx_close(igx_ctx *ctx) {
     for (auto &r : ctx->regex) (void)hipFree(r.second);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->nan_word) (void)hipFree(ctx->nan_word);
+    if (ctx->lsd_status) (void)hipFree(ctx->lsd_status);
     if (ctx->own) (void)hipStreamDestroy(ctx->own);
     delete ctx;
     return IGX_OK;
@@ -656,6 +657,13 @@ extern "C" int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nke
 extern "C" int igx_sort_perm_ex(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                                 const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap, uint32_t *out_perm) {
     return sort_common(ctx, keys, nullptr, nkeys, nrows, pos, valid, out_perm, 0, rowmap);
+}
+
+extern "C" int igx_sort_perm_dn(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows_max,
+                                const uint64_t *d_nrows, const uint64_t *pos, const uint8_t *valid,
+                                const uint32_t *rowmap, uint32_t *out_perm) {
+    if (ctx && !d_nrows) return igx_fail(ctx, IGX_EINVAL, "sort_perm_dn: null device row count");
+    return sort_common(ctx, keys, nullptr, nkeys, nrows_max, pos, valid, out_perm, 0, rowmap, 8, 0, d_nrows);
 }
 
 extern "C" int igx_topk(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,

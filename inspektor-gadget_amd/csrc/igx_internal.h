@@ -29,6 +29,11 @@ struct igx_ctx {
     hipEvent_t handoff = nullptr;
     // the sort's NaN flag: one device word, zero between sorts (k_andor_final clears it)
     uint32_t *nan_word = nullptr;
+    // device-planned LSD passes (k_sort.hip): per-tile digit counts published by tag, so the
+    // array is the context's own (never scratch: a stale word must never carry a live tag)
+    uint64_t *lsd_status = nullptr;
+    size_t lsd_status_words = 0;
+    uint32_t lsd_epoch = 0;
 };
 
 // sets ctx->err and returns code

@@ -1699,7 +1699,8 @@ struct igx_table {
     uint64_t *n_groups = nullptr;
     uint64_t rows_fed = 0;       // rows given to update since the last reset
     bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
-    bool more_probers = false;   // ... on more than MORE_PROBERS_PCT % of its rows
+    bool more_probers = false;   // ... on more than MORE_PROBERS_ON_PM / 1000 of its rows (hysteresis below)
+    uint32_t miss_pm = 0;        // LDS misses per 1000 rows of the last measured cached interval
     uint32_t mode = IGX_GB_AUTO; // igx_groupby_set_mode
     uint32_t direct_left = 0;    // AUTO: intervals to run in the direct form before re-measuring
     uint32_t region_off = 0;     // AUTO: intervals to partition exactly after a region overflowed
@@ -1903,7 +1904,12 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
 
 constexpr size_t GB_LDS_TOTAL = 156 * 1024;    // cache + the two rings (dynamic LDS)
 constexpr uint64_t DIRECT_MISS_PCT = 90;        // AUTO: LDS-miss share that selects the partitioned form
-constexpr uint64_t MORE_PROBERS_PCT = 40;       // LDS-miss share above which a loader wave becomes a prober
+// LDS-miss share (per mille of rows) above which a loader wave becomes a prober, and below
+// which it turns back: a band, so a stream near the threshold does not flip the roles every
+// interval.  Measured: C5 (~42 % misses) 6.15 -> 5.95-6.02 ms with 7 loaders,
+// C2 (~35 %) 3.69 -> 3.86 ms, so C2 keeps 8 -- the band sits between the two.
+constexpr uint64_t MORE_PROBERS_ON_PM = 390;
+constexpr uint64_t MORE_PROBERS_OFF_PM = 370;
 constexpr uint32_t DIRECT_RUN = 16;             // ... for this many intervals
 
 template <class L, bool DBG, int NA>
@@ -2485,9 +2491,8 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.rmask = (1ull << t->rbits) - 1;
     a.max_probe = 1u << t->rbits;
     if (const char *d = std::getenv("IGX_GB_DEBUG")) a.dbg = (uint32_t)std::strtoul(d, nullptr, 0);
-    // one loader wave fewer (one prober more) when the last interval missed the cache on
-    // more than MORE_PROBERS_PCT % of its rows: C5 (≈42 % misses) 6.15 -> 5.95-6.02 ms with 7
-    // loaders, C2 (≈35 %) 3.69 -> 3.86 ms, so C2 keeps 8
+    // one loader wave fewer (one prober more) after intervals that missed the cache on more
+    // than MORE_PROBERS_ON_PM / 1000 of their rows (until one falls below MORE_PROBERS_OFF_PM)
     a.nl = t->more_probers ? NL_DEFAULT - 1 : NL_DEFAULT;
     if (const char *d = std::getenv("IGX_GB_LOADERS")) {   // tuning knob
         const unsigned long v = std::strtoul(d, nullptr, 0);
@@ -2613,7 +2618,8 @@ static int fin_apply(igx_table *t) {
     // row; C4: 4.1 vs 4.4 ms direct, 6.4 ms cached), then one cached interval to measure again.
     if (f.rows_fed >= 1000000 && !f.direct && !f.part) {
         t->prefer_sm = misses * 10 > f.rows_fed * 7;
-        t->more_probers = misses * 100 > f.rows_fed * MORE_PROBERS_PCT;
+        t->miss_pm = (uint32_t)(misses * 1000 / f.rows_fed);
+        t->more_probers = t->miss_pm > (t->more_probers ? MORE_PROBERS_OFF_PM : MORE_PROBERS_ON_PM);
         if (t->mode == IGX_GB_AUTO && misses * 100 > f.rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }
     if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
@@ -2701,6 +2707,8 @@ extern "C" int igx_groupby_info(igx_table *t, igx_groupby_info_t *out) {
     out->part_left = t->direct_left;
     out->exact_left = t->region_off;
     out->sm_probers = t->prefer_sm ? 1u : 0u;
+    out->loaders = t->more_probers ? NL_DEFAULT - 1 : NL_DEFAULT;
+    out->miss_permille = t->miss_pm;
     out->rows = t->rows_fed;
     return IGX_OK;
 }

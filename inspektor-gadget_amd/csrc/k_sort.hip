@@ -18,7 +18,10 @@
 // histogram -> scan -> stable scatter (wave64 ballot multi-split ranks, tile order kept
 // by per-digit running counters in LDS).  Words below the current digit are no longer
 // carried (LSD never reads them again).
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "k_common.h"
@@ -66,8 +69,9 @@ __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, ui
 __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
                                                 uint32_t *__restrict__ payload) {
     const uint64_t i = (uint64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= a.n || (a.d_n && i >= *a.d_n)) return;
-    const uint64_t r = a.reverse ? a.n - 1 - i : i;     // the row composed into slot i
+    const uint64_t n = a.d_n ? min(a.n, *a.d_n) : a.n;
+    if (i >= n) return;
+    const uint64_t r = a.reverse ? n - 1 - i : i;       // the row composed into slot i
     const uint64_t src = a.rowmap ? a.rowmap[r] : r;   // where its values live
     bool nil = a.valid && a.valid[src] == 0;
     uint32_t w = 0;
@@ -532,6 +536,299 @@ __global__ __launch_bounds__(STB) void k_radix_scatter_pf(ScatterArgs a) {
             a.pout[pos] = cp[j];
         }
     }
+}
+
+// ---- device-planned LSD passes (full sorts without float keys, composed keys <= 8 words) ----
+// The same stable LSD order as the host-planned passes above, with no host round trip and one
+// launch per possible byte digit (least significant first).  Each pass kernel decides on the
+// device whether its digit varies -- its global histogram, added up by the pass before it, has
+// no bin holding all n rows -- and, if not, only histograms the next digit and exits (the buffers
+// stay as they are).  An active pass:
+//   - takes a ticket (tile order = dispatch order), loads its tile's rows (the words up to its
+//     own, the payload), ranks every row among its wave's equal digits (multi-split ballots);
+//   - publishes its 256 digit counts as tagged 64-bit words (sc1 stores) and sums the counts of
+//     the tiles before it (sc1 polls of the tags: those tiles hold earlier tickets, so they are
+//     running or done) -- the stable base of each digit in this tile;
+//   - adds the NEXT digit's counts of its rows to that digit's global histogram (rows are only
+//     permuted by a pass, so any tiling gives the same totals; 8 replicas against same-address
+//     serialisation);
+//   - writes its rows through LDS in tile-sorted order, so consecutive lanes store consecutive
+//     addresses of a digit's run instead of scattering one 4-byte store per lane;
+//   - the last tile to finish flips the current-buffer word for the next pass.
+// The first digit's histogram comes from k_lsd_h0; k_lsd_out copies the final payload.  The row
+// count may live on the device (d_n): grids are sized for the upper bound, extra tiles exit.
+// Tags carry (call epoch, pass), so the status words are never cleared.
+constexpr int LSD_MAXW = 8;
+constexpr int LSD_MAXD = 4 * LSD_MAXW;
+constexpr int LSD_REP = 8;   // global histogram replicas per digit
+
+struct LsdCtl {
+    uint32_t cur, err, pad0, pad1;
+    uint32_t ticket[LSD_MAXD];
+    uint32_t done[LSD_MAXD];
+    uint32_t hist[LSD_MAXD][LSD_REP][256];   // per digit, replicated; zeroed per call
+};
+
+// wave64 multi-split: the lanes (of `act`) whose 8-bit digit equals this lane's
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, uint64_t act) {
+    uint64_t peers = act;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+    }
+    return peers;
+}
+
+__device__ __forceinline__ uint32_t lsd_n(uint64_t nmax, const uint64_t *d_n) {
+    return (uint32_t)(d_n ? min(nmax, *d_n) : nmax);
+}
+
+// add the digit counts of this block's rows (LDS h[256], already summed) to replica blockIdx % 8
+__device__ __forceinline__ void lsd_hist_flush(uint32_t *h, LsdCtl *ctl, uint32_t q) {
+    __syncthreads();
+    if (threadIdx.x < 256 && h[threadIdx.x])
+        atomicAdd(&ctl->hist[q][blockIdx.x % LSD_REP][threadIdx.x], h[threadIdx.x]);
+}
+
+// per-row digit -> LDS counts: one add per distinct digit of a wave
+__device__ __forceinline__ void lsd_count(uint32_t *h, uint32_t d, bool ok) {
+    const uint64_t peers = digit_peers(d, __ballot(ok));
+    if (ok && (peers & lanemask_lt()) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+}
+
+// the first digit's histogram: byte 0 of the last (least significant) word
+__global__ __launch_bounds__(STB) void k_lsd_h0(const uint32_t *__restrict__ W, uint32_t KW, uint64_t stride,
+                                                uint64_t nmax, const uint64_t *__restrict__ d_n, LsdCtl *ctl) {
+    __shared__ uint32_t h[256];
+    const uint32_t n = lsd_n(nmax, d_n);
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    if (base >= n) return;
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t *col = W + (uint64_t)(KW - 1) * stride;
+    uint32_t v[SIPT];
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = base + (uint64_t)j * STB + threadIdx.x;
+        v[j] = i < n ? col[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) lsd_count(h, v[j] & 255u, base + (uint64_t)j * STB + threadIdx.x < n);
+    lsd_hist_flush(h, ctl, 0);
+}
+
+struct LsdArgs {
+    uint32_t *W[2];
+    uint32_t *P[2];
+    uint64_t stride, nmax;
+    const uint64_t *d_n;
+    uint64_t *status;     // [tile][256] tagged counts (the context's own array)
+    LsdCtl *ctl;
+    uint32_t KW, pass, tag, pad;
+};
+
+template <int NLMAX>
+__global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
+    __shared__ uint32_t wc[SIPT][STB / 64][256];   // counts, then exclusive offsets inside each digit
+    __shared__ uint32_t gb[256], toff[256], base[256], qsum[4][256], hn[256];
+    __shared__ uint32_t stage[TILE];
+    __shared__ uint8_t sdig[TILE];
+    __shared__ uint32_t tile_s, flags;
+    const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const uint32_t n = lsd_n(a.nmax, a.d_n);
+    const uint32_t p = a.pass, ND = 4 * a.KW;
+    const uint32_t w = a.KW - 1 - p / 4, shift = 8 * (p % 4);
+    const bool has_next = p + 1 < ND;
+    const uint32_t wn = a.KW - 1 - (p + 1) / 4, shn = 8 * ((p + 1) % 4);   // the next digit
+    // this digit's global histogram (summed replicas): constant iff one bin holds all n rows
+    if (t == 0) flags = 0;
+    if (t < 256) hn[t] = 0;
+    __syncthreads();
+    if (t < 256) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < LSD_REP; ++r) c += a.ctl->hist[p][r][t];
+        gb[t] = c;
+        if (c == n) flags = 1;
+    }
+    __syncthreads();
+    const uint32_t cur = a.ctl->cur;
+    if (flags || n < 2) {
+        // inactive: only the next digit's histogram (over this block's rows of the unchanged buffer)
+        const uint64_t tb = (uint64_t)blockIdx.x * TILE;
+        if (!has_next || tb >= n || n < 2) return;
+        const uint32_t *col = a.W[cur] + (uint64_t)wn * a.stride;
+#pragma unroll
+        for (int j = 0; j < SIPT; ++j) {
+            const uint64_t i = tb + (uint64_t)j * STB + t;
+            lsd_count(hn, i < n ? (col[i] >> shn) & 255u : 0u, i < n);
+        }
+        lsd_hist_flush(hn, a.ctl, p + 1);
+        return;
+    }
+    // global exclusive base of each digit value (256-thread scan of gb)
+    if (t < 256) {
+        const uint32_t c = gb[t];
+        uint32_t inc = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if ((int)lane >= d) inc += y;
+        }
+        if (lane == 63) qsum[0][wave] = inc;
+        base[t] = inc - c;
+    }
+    if (t == 0) tile_s = atomicAdd(&a.ctl->ticket[p], 1u);
+    for (uint32_t i = t; i < SIPT * (STB / 64) * 256; i += STB) (&wc[0][0][0])[i] = 0;
+    __syncthreads();
+    if (t < 256) {
+        for (uint32_t q = 0; q < wave; ++q) base[t] += qsum[0][q];
+        gb[t] = base[t];   // keep: the global base of digit t
+    }
+    __syncthreads();   // qsum is rewritten by the predecessor sums below
+    const uint32_t tile = tile_s;
+    const uint32_t ntiles = (n + TILE - 1) / TILE;
+    if (tile >= ntiles) return;
+    const uint32_t nl = w + 1;   // every word up to this one is carried
+    const uint64_t tbase = (uint64_t)tile * TILE;
+    uint32_t cw[SIPT][NLMAX], cp[SIPT], dg[SIPT], rk[SIPT];
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const uint64_t i = tbase + (uint64_t)j * STB + t;
+        if (i < n) {
+#pragma unroll
+            for (int l = 0; l < NLMAX; ++l)
+                if ((uint32_t)l < nl) cw[j][l] = a.W[cur][(uint64_t)l * a.stride + i];
+            cp[j] = a.P[cur][i];
+        }
+    }
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        const bool valid = tbase + (uint64_t)j * STB + t < n;
+        uint32_t dv = 0, dvn = 0;
+#pragma unroll
+        for (int l = 0; l < NLMAX; ++l) {
+            if ((uint32_t)l == w) dv = cw[j][l];
+            if ((uint32_t)l == wn) dvn = cw[j][l];
+        }
+        dg[j] = valid ? (dv >> shift) & 255u : 0u;
+        const uint64_t peers = digit_peers(dg[j], __ballot(valid));
+        rk[j] = (uint32_t)__popcll(peers & lt);
+        if (valid && rk[j] == 0) wc[j][wave][dg[j]] = (uint32_t)__popcll(peers);
+        if (has_next) lsd_count(hn, valid ? (dvn >> shn) & 255u : 0u, valid);
+    }
+    __syncthreads();
+    if (t < 256) {   // (sub-row, wave) order is the tile's row order: the stable offsets
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < SIPT; ++j) {
+#pragma unroll
+            for (int v = 0; v < STB / 64; ++v) {
+                const uint32_t x = wc[j][v][t];
+                wc[j][v][t] = r;
+                r += x;
+            }
+        }
+        __hip_atomic_store(&a.status[(uint64_t)tile * 256 + t], ((uint64_t)a.tag << 32) | r, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        toff[t] = r;   // the tile's count of digit t (scanned below)
+        if (has_next && hn[t]) atomicAdd(&a.ctl->hist[p + 1][tile % LSD_REP][t], hn[t]);
+    }
+    // the counts of the tiles before this one: four quarters of 256 threads, one digit each
+    {
+        const uint32_t d = t & 255u, q = t >> 8;
+        const uint32_t q0 = tile * q / 4, q1 = tile * (q + 1) / 4;
+        uint32_t sum = 0;
+        for (uint32_t j = q0; j < q1; j += 8) {   // 8 polls in flight per thread
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = j + u < q1 ? __hip_atomic_load(&a.status[(uint64_t)(j + u) * 256 + d], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : (uint64_t)a.tag << 32;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                uint32_t spins = 0;
+                while ((uint32_t)(v[u] >> 32) != a.tag) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) {   // never expected: a tile before this one holds an earlier ticket
+                        atomicOr(&a.ctl->err, 1u);
+                        break;
+                    }
+                    v[u] = __hip_atomic_load(&a.status[(uint64_t)(j + u) * 256 + d], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                }
+                sum += (uint32_t)v[u];
+            }
+        }
+        qsum[q][d] = sum;
+    }
+    __syncthreads();
+    if (t < 256) {
+        // where digit t's run starts in this tile's LDS order (exclusive scan of the tile counts),
+        // and where it goes: the digit's global base + the tiles before this one
+        const uint32_t c = toff[t];
+        uint32_t inc = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if ((int)lane >= d) inc += y;
+        }
+        base[t] = gb[t] + qsum[0][t] + qsum[1][t] + qsum[2][t] + qsum[3][t];
+        gb[t] = inc - c;   // wave-local exclusive start (gb is free now)
+        if (lane == 63) hn[wave] = inc;   // wave totals (hn is free now)
+    }
+    __syncthreads();
+    if (t < 256) {
+        uint32_t add = 0;
+        for (uint32_t q = 0; q < wave; ++q) add += hn[q];
+        toff[t] = gb[t] + add;
+    }
+    __syncthreads();
+    // tile-sorted LDS position of each row, then every carried word and the payload staged
+    uint32_t lp[SIPT];
+#pragma unroll
+    for (int j = 0; j < SIPT; ++j) {
+        lp[j] = toff[dg[j]] + wc[j][wave][dg[j]] + rk[j];
+        if (tbase + (uint64_t)j * STB + t < n) sdig[lp[j]] = (uint8_t)dg[j];
+    }
+    const uint32_t tn = min<uint32_t>(TILE, n - (uint32_t)tbase);
+    for (uint32_t l = 0; l <= nl; ++l) {   // l == nl: the payload
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SIPT; ++j) {
+            if (tbase + (uint64_t)j * STB + t < n) {
+                uint32_t x = cp[j];
+#pragma unroll
+                for (int m = 0; m < NLMAX; ++m)
+                    if ((uint32_t)m == l && l < nl) x = cw[j][m];   // l == nl: the payload
+                stage[lp[j]] = x;
+            }
+        }
+        __syncthreads();
+        uint32_t *out = l < nl ? a.W[cur ^ 1] + (uint64_t)l * a.stride : a.P[cur ^ 1];
+        for (uint32_t i = t; i < tn; i += STB) {
+            const uint32_t d = sdig[i];
+            out[base[d] + i - toff[d]] = stage[i];
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        if (atomicAdd(&a.ctl->done[p], 1u) == ntiles - 1) a.ctl->cur = cur ^ 1;   // the next pass reads what this wrote
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lsd_out(uint32_t *const P0, uint32_t *const P1, const LsdCtl *__restrict__ ctl,
+                                                 uint64_t nmax, const uint64_t *__restrict__ d_n, uint32_t limit,
+                                                 uint32_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t n = min<uint64_t>(lsd_n(nmax, d_n), limit ? limit : nmax);
+    if (i >= n) return;
+    out[i] = ctl->err ? 0xFFFFFFFFu : (ctl->cur ? P1 : P0)[i];   // a failed wait poisons the result
 }
 
 // ---- top-K by radix select (k <= SEL_SMALL_K) -----------------------------------------
@@ -1132,16 +1429,45 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     constexpr uint32_t ANDOR_BLOCKS = 256;
     const size_t res_b = igx_align((size_t)KW * 8 + 4, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
-    if (d_nrows && !(use_sel && !any_float && rowmap && !valid))   // only the device selection reads the count there
-        return igx_fail(ctx, IGX_EINVAL, "sort: a device row count needs a top-K without float keys or nil mask");
+    // Full sorts without float keys may plan their passes on the device (k_lsd_*: no host read at
+    // all) with IGX_SORT_DEVPLAN=1.  Measured on C1 (1M rows, 16 live digits) they are slower
+    // than the host-planned passes (0.55-0.61 vs 0.46 ms), so the default is the
+    // host plan: one read-back of the AND/OR words -- and of a device row count, when there is
+    // one -- per sort.
+    const bool use_lsd = !use_sel && !any_float && KW > 0 && KW <= (uint32_t)LSD_MAXW &&
+                         std::getenv("IGX_SORT_DEVPLAN") != nullptr;
+    if (d_nrows && (any_float || (use_sel && !(rowmap && !valid))))
+        return igx_fail(ctx, IGX_EINVAL, "sort: a device row count needs integer or string keys (and, for a top-K, "
+                                         "a slot list and no nil mask)");
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     static_assert(sizeof(SelState) <= 64 * 4, "SelState fits the 64 words before the selection histogram");
     if (!ctx->nan_word) {
         IGX_HIP(ctx, hipMalloc(&ctx->nan_word, 64));
         IGX_HIP(ctx, hipMemsetAsync(ctx->nan_word, 0, 64, ctx->stream));
     }
+    const size_t lsd_b = use_lsd ? igx_align(sizeof(LsdCtl), 256) : 0;
+    if (use_lsd) {
+        // the tagged per-tile counts: the context's own array, zeroed when it grows and when the
+        // epoch wraps, so a word of an earlier call never carries a live tag
+        const size_t need = (size_t)nblocks * 256;
+        if (need > ctx->lsd_status_words) {
+            IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->lsd_status) (void)hipFree(ctx->lsd_status);
+            ctx->lsd_status = nullptr;
+            ctx->lsd_status_words = 0;
+            const size_t want = std::max(need, (size_t)256 * 256);
+            IGX_HIP(ctx, hipMalloc(&ctx->lsd_status, want * 8));
+            IGX_HIP(ctx, hipMemsetAsync(ctx->lsd_status, 0, want * 8, ctx->stream));
+            ctx->lsd_status_words = want;
+            ctx->lsd_epoch = 0;
+        }
+        if (++ctx->lsd_epoch >= (1u << 26)) {
+            IGX_HIP(ctx, hipMemsetAsync(ctx->lsd_status, 0, ctx->lsd_status_words * 8, ctx->stream));
+            ctx->lsd_epoch = 1;
+        }
+    }
     void *s;
-    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b, &s);
+    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b + lsd_b, &s);
     if (rc) return rc;
     char *c = reinterpret_cast<char *>(s);
     uint32_t *W[2] = {reinterpret_cast<uint32_t *>(c), reinterpret_cast<uint32_t *>(c + words_b)};
@@ -1170,6 +1496,36 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     if (KW == 0) {   // no key and no position words: the (possibly reversed) row order itself
         const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
         IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[0], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        IGX_HIP(ctx, hipGetLastError());
+        return IGX_OK;
+    }
+    if (use_lsd) {
+        LsdCtl *ctl = reinterpret_cast<LsdCtl *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b);
+        IGX_HIP(ctx, hipMemsetAsync(ctl, 0, sizeof(LsdCtl), ctx->stream));
+        hipLaunchKernelGGL(k_lsd_h0, dim3(nblocks), dim3(STB), 0, ctx->stream, W[0], KW, stride, nrows, d_nrows, ctl);
+        LsdArgs la{};
+        la.W[0] = W[0];
+        la.W[1] = W[1];
+        la.P[0] = P[0];
+        la.P[1] = P[1];
+        la.stride = stride;
+        la.nmax = nrows;
+        la.d_n = d_nrows;
+        la.status = ctx->lsd_status;
+        la.ctl = ctl;
+        la.KW = KW;
+        for (uint32_t p = 0; p < KW * 4; ++p) {
+            la.pass = p;
+            la.tag = (ctx->lsd_epoch << 5) | p;
+            // pass p works on word KW-1-p/4 and carries the words up to it
+            if (KW - p / 4 <= 4)
+                hipLaunchKernelGGL(k_lsd_pass<4>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
+            else
+                hipLaunchKernelGGL(k_lsd_pass<8>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
+        }
+        const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+        hipLaunchKernelGGL(k_lsd_out, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, P[0], P[1], ctl,
+                           nrows, d_nrows, limit, out_perm);
         IGX_HIP(ctx, hipGetLastError());
         return IGX_OK;
     }
@@ -1207,9 +1563,11 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res, ctx->nan_word,
                        nullptr, nrows, limit, nullptr, nullptr);
     uint32_t *hres;
-    rc = igx_pinned(ctx, KW * 8 + 4, reinterpret_cast<void **>(&hres));
+    rc = igx_pinned(ctx, KW * 8 + 16, reinterpret_cast<void **>(&hres));
     if (rc) return rc;
     IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8 + 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (d_nrows)   // the device row count rides the same read-back
+        IGX_HIP(ctx, hipMemcpyAsync(hres + 2 * KW + 2, d_nrows, 8, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     // Go's `<` is unordered on NaN, so getLessFunc (sort.go:125-135) is no strict weak order
     // once a NaN is present and SliceStable's result depends on its insertion-sort blocks and
@@ -1277,6 +1635,13 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         return IGX_OK;
     }
 
+    if (d_nrows) {   // the slice's length, read back with the AND/OR words
+        uint64_t dn;
+        std::memcpy(&dn, hres + 2 * KW + 2, 8);
+        nrows = std::min<uint64_t>(nrows, dn);
+        if (nrows == 0) return IGX_OK;
+    }
+    const uint32_t pblocks = (uint32_t)((nrows + TILE - 1) / TILE);
     // digit plan: word w (0 = most significant), byte b (0 = least significant in word)
     std::vector<int> live_word(KW, 0);
     for (uint32_t w = 0; w < KW; ++w) live_word[w] = (hres[2 * w] ^ hres[2 * w + 1]) != 0;
@@ -1297,7 +1662,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         }
         sa.nlive = nl;
         sa.dword = dslot;
-        sa.nblocks = nblocks;
+        sa.nblocks = pblocks;
         sa.n = nrows;
         sa.off = hist;
         for (int b = 0; b < 4; ++b) {
@@ -1305,18 +1670,18 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             sa.shift = 8 * b;
             sa.pin = P[cur];
             sa.pout = P[cur ^ 1];
-            const bool scan_free = nl <= 8 && nblocks <= SCAN_FREE_TILES;
-            hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(STB), 0, ctx->stream,
-                               sa.in[dslot], sa.shift, nrows, nblocks, hist, scan_free ? 1u : 0u);
+            const bool scan_free = nl <= 8 && pblocks <= SCAN_FREE_TILES;
+            hipLaunchKernelGGL(k_radix_hist, dim3(pblocks), dim3(STB), 0, ctx->stream,
+                               sa.in[dslot], sa.shift, nrows, pblocks, hist, scan_free ? 1u : 0u);
             sa.off = scan_free ? nullptr : hist;
             sa.cnt = hist;
-            if (!scan_free) launch_scan(ctx->stream, hist, (uint64_t)256 * nblocks, scan_part);
+            if (!scan_free) launch_scan(ctx->stream, hist, (uint64_t)256 * pblocks, scan_part);
             if (nl <= 4)
-                hipLaunchKernelGGL(k_radix_scatter_pf<4>, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter_pf<4>, dim3(pblocks), dim3(STB), 0, ctx->stream, sa);
             else if (nl <= 8)
-                hipLaunchKernelGGL(k_radix_scatter_pf<8>, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter_pf<8>, dim3(pblocks), dim3(STB), 0, ctx->stream, sa);
             else
-                hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(STB), 0, ctx->stream, sa);
+                hipLaunchKernelGGL(k_radix_scatter, dim3(pblocks), dim3(STB), 0, ctx->stream, sa);
             // swap buffers: the next pass reads what this one wrote
             cur ^= 1;
             for (uint32_t l = 0; l < nl; ++l) {

@@ -113,12 +113,13 @@ def gen_file(seed, rank, G, cdf, base, n):
 # ------------------------------------------------------------------------------------
 # filter
 # ------------------------------------------------------------------------------------
-def filter_rows(cols, preds, n, valid=None, any=False, nil_match=False):
+def filter_rows(cols, preds, n, valid=None, any=False, nil_match=False, device_count=False):
     """cols: list of device tensors (indexed by Pred.col); preds: list of Pred.
     any=False: AND (MatchAll); any=True: OR (MatchAny); any number of preds.
     nil_match=False: nil rows (valid == 0) are skipped (FilterEntries, filter.go:310-314);
     True: a nil row evaluates Match(nil) == negate per pred (filter.go:286-291).
-    Returns (idx u32 tensor of length n_selected)."""
+    Returns (idx u32 tensor of length n_selected); with device_count=True, (idx of capacity n,
+    count u64 device tensor) and no host synchronisation."""
     torch = torch_mod()
     ctx = context()
     dev = cols[0].device if cols else (valid.device if valid is not None else "cuda")
@@ -129,6 +130,8 @@ def filter_rows(cols, preds, n, valid=None, any=False, nil_match=False):
     flags = (_abi.FILTER_ANY if any else 0) | (_abi.FILTER_NIL_MATCH if nil_match else 0)
     ctx.check(ctx.L.igx_filter_ex(ctx.h, ccols, len(cols), cpreds, len(preds), ptr(valid), n, flags,
                                   ptr(out), ptr(cnt)))
+    if device_count:
+        return out, cnt
     k = int(cnt.item())
     return out[:k]
 
@@ -165,10 +168,13 @@ def take(tensors, idx, nrows=None, pad=False):
 # ------------------------------------------------------------------------------------
 # sort
 # ------------------------------------------------------------------------------------
-def sort_perm(keys, n, pos=None, valid=None, k=None, rowmap=None):
+def sort_perm(keys, n, pos=None, valid=None, k=None, rowmap=None, d_count=None):
     """keys: list of (tensor, desc) in sortBy order.  Returns u32 permutation (first k).
     rowmap (u32, n rows): sort the selection vector -- row i is row rowmap[i] of the key
-    columns, valid and pos (igx_sort_perm_ex); the result is then rowmap values in order."""
+    columns, valid and pos (igx_sort_perm_ex); the result is then rowmap values in order.
+    d_count (u64 device tensor, with rowmap): the slice is rowmap[:d_count], n its upper bound
+    (igx_sort_perm_dn: no host round trip); the result has capacity n, its first d_count
+    entries sorted."""
     torch = torch_mod()
     ctx = context()
     dev = keys[0][0].device if keys else (pos.device if pos is not None else "cuda")
@@ -186,7 +192,11 @@ def sort_perm(keys, n, pos=None, valid=None, k=None, rowmap=None):
     if rowmap is not None:
         if k is not None:
             raise ValueError("a top-K over a selection vector: sort the view first")
-        ctx.check(ctx.L.igx_sort_perm_ex(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(rowmap), ptr(out)))
+        if d_count is not None:
+            ctx.check(ctx.L.igx_sort_perm_dn(ctx.h, arr, len(sk), n, ptr(d_count), ptr(pos), ptr(valid),
+                                             ptr(rowmap), ptr(out)))
+        else:
+            ctx.check(ctx.L.igx_sort_perm_ex(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(rowmap), ptr(out)))
     elif k is None:
         ctx.check(ctx.L.igx_sort_perm(ctx.h, arr, len(sk), n, ptr(pos), ptr(valid), ptr(out)))
     else:

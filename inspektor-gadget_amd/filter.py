@@ -105,5 +105,11 @@ def FilterEntries(cols: Columns, batch, filters):
         return None
     # The reference narrows `entries` filter by filter (:301-322); the rows left at the end
     # are the non-nil rows every filter matches, in input order -- one AND scan and one
-    # compaction here.  (A parse error returns before any result either way.)
+    # compaction here.  (A parse error returns before any result either way.)  Over a plain
+    # batch the result is a view whose length stays on the device until asked for (len(),
+    # .n): SortEntries of it then runs without a host round trip.
+    if batch.sel is None:
+        idx, cnt = engine.filter_rows(batch.tensors_in_schema_order(), [s.pred for s in specs], batch.n,
+                                      batch.valid, device_count=True)
+        return EventBatch(batch.cols, batch._base, batch._base_valid, sel=idx, sel_count=cnt)
     return batch.take(_scan(batch, specs))

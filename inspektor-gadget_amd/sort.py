@@ -61,7 +61,22 @@ class ColumnSorterCollection:
         """Returns the batch in sorted order (the reference sorts []*T in place).  A view (a
         filtered slice of pointers) is sorted through its selection vector: the result is the
         same entries' row ids in sorted order, no column read beyond the sort keys."""
-        if batch is None or batch.n == 0:
+        if batch is None:
+            return batch
+        pend = batch.pending() if pos is None else None
+        if pend is not None:   # a selection whose length is on the device: sorted there, no round trip
+            sel, cnt = pend
+            base, base_valid = batch._base, batch._base_valid
+            ordered = self.cols.GetOrderedColumns()
+            keys = [(base[ordered[sk.col].Name.lower()], bool(sk.desc), sk.kind) for sk in self.keys]
+            if keys and self._device_countable(keys):
+                if sel.shape[0] == 0:
+                    return batch
+                out = engine.sort_perm_kinds(keys, int(sel.shape[0]), valid=base_valid, rowmap=sel.contiguous(),
+                                             d_count=cnt)
+                return EventBatch(batch.cols, base, base_valid, sel=out, sel_count=cnt)
+            # otherwise the synchronous path below (n read on the host)
+        if batch.n == 0:
             return batch
         base, base_valid, sel = batch.base()
         if sel is None or pos is not None:
@@ -72,6 +87,13 @@ class ColumnSorterCollection:
             sel = sel.to(torch_mod().int32)
         out = engine.sort_perm_kinds(keys, batch.n, valid=base_valid, rowmap=sel.contiguous())
         return EventBatch(batch.cols, base, base_valid, sel=out)
+
+
+    @staticmethod
+    def _device_countable(keys):
+        """igx_sort_perm_dn's shape: no float key (a NaN takes the exact Go path, which needs the
+        length on the host)."""
+        return all(kind != _abi.KIND_FLOAT for _, _, kind in keys)
 
 
 def Prepare(cols: Columns, sort_by) -> ColumnSorterCollection:

@@ -31,6 +31,7 @@
  *      pkg/gadgets/top/tcp/tracer/tracer.go:147-253, pkg/gadgets/top/top.go:39-41
  */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -961,4 +962,193 @@ void or_hist_log2_mt(const u32 *dev, const u32 *cont, const i64 *delta, u64 n, c
     for (u32 t = 0; t < T; t++)
         for (u64 x = 0; x < keys; x++) hist[x] += priv[(u64)t * keys + x];
     free(priv); free(th); free(a);
+}
+
+/* ---------------------------------------------------------------------------------------
+ * §8: advise network-policy's GeneratePolicies on STRING keys, the reference's own shape
+ * (pkg/gadgets/advise/networkpolicy/advisor/advisor.go): per event the filter (:282-292),
+ * localPodKey = Namespace + ":" + labelKeyString(PodLabels) (:143-145, labelKeyString :132-141
+ * sorts the label keys left after LabelsToIgnore :36-40, :104-116), eventsBySource[key] append
+ * (:294-299); then per source, networkPeerKey (:147-158, fmt.Sprintf("%s:%d", ..., Port)) and
+ * first-event-wins egress / ingress maps (:302-320).  Returns the number of (source, direction,
+ * peer key) entries -- the distinct tuples the device table holds.  Timed as C4's faithful CPU
+ * baseline (bench.py); single-threaded like GeneratePolicies.
+ *
+ * The synthetic C4 stream carries integer ids (or_gen_np); the strings a Kubernetes event would
+ * carry are derived from them, one-to-one: source s -> Namespace "ns-<s%50>", PodLabels
+ * {app: "app-<s>", pod-template-hash: <hash>, tier: "tier-<s%4>"}; peer p -> RemoteKind pod /
+ * svc / other by p%3, RemoteNamespace "ns-<p%50>", RemoteLabels {app: "peer-<p>", pod-template-
+ * hash: <hash>}, and for "other" the peer's canonical address 10.96.x.y (the stream's RemoteAddr
+ * of that peer).  Go also copies each whole Event into eventsBySource; here the event index is
+ * appended (cheaper than the reference).
+ * --------------------------------------------------------------------------------------- */
+typedef struct { const char *k; char v[24]; } np_label;
+
+static int np_label_cmp(const void *a, const void *b) {
+    return strcmp(((const np_label *)a)->k, ((const np_label *)b)->k);
+}
+
+static int np_ignored(const char *k) {   /* defaultLabelsToIgnore, advisor.go:36-40 */
+    return !strcmp(k, "controller-revision-hash") || !strcmp(k, "pod-template-generation") ||
+           !strcmp(k, "pod-template-hash");
+}
+
+/* labelKeyString: the labels not ignored, keys sorted, "k=v" joined by "," */
+static int np_label_key_string(np_label *L, int nl, char *out) {
+    np_label keep[4];
+    int m = 0;
+    for (int i = 0; i < nl; i++)
+        if (!np_ignored(L[i].k)) keep[m++] = L[i];
+    qsort(keep, m, sizeof(np_label), np_label_cmp);
+    int len = 0;
+    for (int i = 0; i < m; i++) len += sprintf(out + len, "%s%s=%s", i ? "," : "", keep[i].k, keep[i].v);
+    return len;
+}
+
+static int np_pod_labels(u32 id, const char *app_prefix, int with_tier, np_label *L) {
+    int n = 0;
+    L[n].k = "app"; snprintf(L[n].v, sizeof L[n].v, "%s-%u", app_prefix, id); n++;
+    L[n].k = "pod-template-hash"; snprintf(L[n].v, sizeof L[n].v, "%08x", (u32)sm64(id ^ 0xABCD)); n++;
+    if (with_tier) { L[n].k = "tier"; snprintf(L[n].v, sizeof L[n].v, "tier-%u", id % 4); n++; }
+    return n;
+}
+
+static int np_local_pod_key(u32 s, char *out) {   /* localPodKey, advisor.go:143-145 */
+    np_label L[4];
+    const int nl = np_pod_labels(s, "app", 1, L);
+    int len = sprintf(out, "ns-%u:", s % 50);
+    return len + np_label_key_string(L, nl, out + len);
+}
+
+static int np_peer_key(u32 p, u16 port, char *out) {   /* networkPeerKey, advisor.go:147-158 */
+    char ret[160];
+    int len;
+    if (p % 3 == 0 || p % 3 == 1) {   /* RemoteKindPod / RemoteKindService */
+        np_label L[4];
+        const int nl = np_pod_labels(p, "peer", 0, L);
+        len = sprintf(ret, "%s:ns-%u:", p % 3 == 0 ? "pod" : "svc", p % 50);
+        len += np_label_key_string(L, nl, ret + len);
+    } else {                          /* RemoteKindOther: the peer's address */
+        const u32 a = 0x0a600000u | (p & 0xfffff);
+        len = sprintf(ret, "other:%u.%u.%u.%u", a >> 24, (a >> 16) & 255, (a >> 8) & 255, a & 255);
+    }
+    (void)len;
+    return sprintf(out, "%s:%u", ret, (unsigned)port);
+}
+
+/* string-keyed open-addressing table: keys in a byte pool, FNV-1a hashes, generation-cleared */
+typedef struct {
+    u64 cap, n;
+    u64 *h; u64 *off; u32 *len; u32 *gen; u32 *val;
+    char *pool; u64 pool_len, pool_cap;
+    u32 cur_gen;
+} np_smap;
+
+static u64 np_fnv(const char *s, u32 len) {
+    u64 h = 14695981039346656037ull;
+    for (u32 i = 0; i < len; i++) { h ^= (u8)s[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+static void np_smap_init(np_smap *m, u64 cap) {
+    memset(m, 0, sizeof *m);
+    m->cap = 1; while (m->cap < cap * 2) m->cap <<= 1;
+    m->h = (u64 *)malloc(m->cap * 8); m->off = (u64 *)malloc(m->cap * 8);
+    m->len = (u32 *)malloc(m->cap * 4); m->gen = (u32 *)calloc(m->cap, 4); m->val = (u32 *)malloc(m->cap * 4);
+    m->pool_cap = 1 << 20; m->pool = (char *)malloc(m->pool_cap);
+    m->cur_gen = 1;
+}
+
+static void np_smap_free(np_smap *m) {
+    free(m->h); free(m->off); free(m->len); free(m->gen); free(m->val); free(m->pool);
+}
+
+static void np_smap_clear(np_smap *m) { m->cur_gen++; m->n = 0; m->pool_len = 0; }
+
+/* index of key, inserting it with val when absent (*added = 1) */
+static u32 np_smap_get(np_smap *m, const char *k, u32 len, u32 val, int *added) {
+    const u64 h = np_fnv(k, len);
+    u64 i = h & (m->cap - 1);
+    for (;; i = (i + 1) & (m->cap - 1)) {
+        if (m->gen[i] != m->cur_gen) break;
+        if (m->h[i] == h && m->len[i] == len && !memcmp(m->pool + m->off[i], k, len)) {
+            *added = 0;
+            return m->val[i];
+        }
+    }
+    if (m->pool_len + len > m->pool_cap) {
+        while (m->pool_len + len > m->pool_cap) m->pool_cap *= 2;
+        m->pool = (char *)realloc(m->pool, m->pool_cap);
+    }
+    memcpy(m->pool + m->pool_len, k, len);
+    m->gen[i] = m->cur_gen; m->h[i] = h; m->off[i] = m->pool_len; m->len[i] = len; m->val[i] = val;
+    m->pool_len += len;
+    m->n++;
+    *added = 1;
+    return val;
+}
+
+u64 or_np_advise_strings(const u32 *src, const u32 *peer, const u16 *port, const u8 *pkt, const u8 *typ,
+                         const u32 *hostip, const u32 *raddr, u64 n) {
+    /* pass 1: eventsBySource (map[string][]Event; here an index list per source) */
+    np_smap bysrc;
+    np_smap_init(&bysrc, 1 << 16);
+    u64 nsrc_cap = 1 << 12, nsrc = 0;
+    u64 *cnt = (u64 *)calloc(nsrc_cap, 8);
+    u32 *ev_src = (u32 *)malloc((n ? n : 1) * 4);
+    char key[256];
+    for (u64 i = 0; i < n; i++) {
+        ev_src[i] = 0xFFFFFFFFu;
+        if (typ[i] != 0) continue;                                  /* :283-285 */
+        if (pkt[i] != 0 && pkt[i] != 4) continue;                   /* :286-288 HOST / OUTGOING */
+        if (pkt[i] == 0 && hostip[i] == raddr[i]) continue;         /* :290-292 */
+        const int len = np_local_pod_key(src[i], key);
+        if (bysrc.n * 2 >= bysrc.cap) {   /* grow: rehash into a bigger table */
+            np_smap big;
+            np_smap_init(&big, bysrc.cap);
+            for (u64 j = 0; j < bysrc.cap; j++)
+                if (bysrc.gen[j] == bysrc.cur_gen) {
+                    int ad;
+                    np_smap_get(&big, bysrc.pool + bysrc.off[j], bysrc.len[j], bysrc.val[j], &ad);
+                }
+            np_smap_free(&bysrc);
+            bysrc = big;
+        }
+        int added;
+        const u32 sidx = np_smap_get(&bysrc, key, (u32)len, (u32)nsrc, &added);
+        if (added) {
+            if (++nsrc > nsrc_cap) { cnt = (u64 *)realloc(cnt, nsrc_cap * 2 * 8); memset(cnt + nsrc_cap, 0, nsrc_cap * 8); nsrc_cap *= 2; }
+        }
+        ev_src[i] = sidx;
+        cnt[sidx]++;
+    }
+    /* group the event indices by source, in event order (the appended slices) */
+    u64 *start = (u64 *)calloc(nsrc + 1, 8);
+    for (u64 s = 0; s < nsrc; s++) start[s + 1] = start[s] + cnt[s];
+    u64 *fill = (u64 *)malloc((nsrc + 1) * 8);
+    memcpy(fill, start, (nsrc + 1) * 8);
+    u32 *evs = (u32 *)malloc((start[nsrc] ? start[nsrc] : 1) * 4);
+    for (u64 i = 0; i < n; i++)
+        if (ev_src[i] != 0xFFFFFFFFu) evs[fill[ev_src[i]]++] = (u32)i;
+    /* pass 2: per source, egressNetworkPeer / ingressNetworkPeer (first event wins) */
+    np_smap eg, in;
+    np_smap_init(&eg, 1 << 10);
+    np_smap_init(&in, 1 << 10);
+    u64 total = 0;
+    for (u64 s = 0; s < nsrc; s++) {
+        const u64 m = start[s + 1] - start[s];
+        if (eg.cap < m * 2) { np_smap_free(&eg); np_smap_free(&in); np_smap_init(&eg, m); np_smap_init(&in, m); }
+        np_smap_clear(&eg);
+        np_smap_clear(&in);
+        for (u64 x = start[s]; x < start[s + 1]; x++) {
+            const u32 i = evs[x];
+            const int len = np_peer_key(peer[i], port[i], key);
+            int added;
+            np_smap_get(pkt[i] == 4 ? &eg : &in, key, (u32)len, i, &added);
+        }
+        total += eg.n + in.n;
+    }
+    np_smap_free(&bysrc); np_smap_free(&eg); np_smap_free(&in);
+    free(cnt); free(ev_src); free(start); free(fill); free(evs);
+    return total;
 }

@@ -81,6 +81,8 @@ def _declare(L):
     L.or_groupby_topk_mt.restype = u64
     L.or_hist_log2_mt.argtypes = [vp, vp, vp, u64, vp, C.c_uint32, C.c_uint32, u64, C.c_uint32, vp,
                                   C.c_uint32]
+    L.or_np_advise_strings.argtypes = [vp] * 7 + [u64]
+    L.or_np_advise_strings.restype = u64
 
 
 # ------------------------------------------------------------------------------------
@@ -643,6 +645,14 @@ def np_mark(ev):
     OUTGOING (4), and not (HOST and PodHostIP == RemoteAddr)."""
     t, p = ev["type"], ev["pkt"]
     return (t == 0) & ((p == 0) | (p == 4)) & ~((p == 0) & (ev["hostip"] == ev["raddr"]))
+
+
+def np_advise_strings(ev):
+    """or_np_advise_strings: GeneratePolicies' dedup on the reference's own string keys
+    (advisor.go:130-159 key building, :279-320 maps) over an or_gen_np batch; returns the number
+    of (source, direction, peer) entries = the distinct tuples of the device table."""
+    cols = [np.ascontiguousarray(ev[k]) for k in ("src", "peer", "port", "pkt", "type", "hostip", "raddr")]
+    return int(lib().or_np_advise_strings(*[_p(c) for c in cols], len(cols[0])))
 
 
 def pad_keys(batch, names):

@@ -106,3 +106,13 @@ def test_device_dedup_end_to_end(igx, oracle):
     adv.LoadBuffer(json.dumps(ev))
     adv.GeneratePolicies()
     assert adv.Policies == oracle.advisor_policies(ev)
+
+
+def test_string_keyed_generate_policies_counts_the_device_tuples(oracle):
+    """C4's CPU baseline (or_np_advise_strings: GeneratePolicies on localPodKey / networkPeerKey
+    strings, advisor.go:130-159, 279-320) keeps exactly the (source, direction, peer, port)
+    tuples the device's distinct table counts on the same stream."""
+    h = oracle.gen_np(0xC4, 10_000, 100_000, 0, 300_000)
+    keys = oracle.pad_keys(h, ("src", "pkt", "peer", "port"))
+    k, _, _ = oracle.groupby(keys, [], valid=oracle.np_mark(h))
+    assert oracle.np_advise_strings(h) == k.shape[0] > 250_000

@@ -177,3 +177,44 @@ def test_bench_c5_async_intervals_match_oracle(igx, torch):
     assert ck["groups_equal"] and ck["table_checksum_equal"] and ck["topk_equal"], ck
     assert ck["bit_exact"] is True
     torch.cuda.empty_cache()
+
+
+def test_auto_loader_choice_has_a_band(igx, torch):
+    """AUTO's cached-form wave roles (igx_groupby_info: loaders, miss_permille): C2's stream
+    (~35 % LDS misses) keeps 8 loader waves over 5 intervals; C5's (~42 %) moves to 7 after its
+    first interval and stays there -- the switch has a band (on above 39 %, off below 37 %)."""
+    E, H, A = igx.engine, igx.columns, igx._abi
+    bench = importlib.import_module("bench")
+    cdf = E.zipf_cdf(G, 1.1)
+    ev = E.gen_tcp(0xC2, 0, G, H.to_device(cdf), 0, N)
+    cols = [ev[k] for k in bench.TCP_NAMES] + [ev["size"].view(torch.int32)]
+    tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2], [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)],
+                  G + G // 4)
+    c2 = []
+    for _ in range(5):
+        tab.reset()
+        tab.update(cols, list(range(8)), N, 0, [bench.family_in_pred(A, 7), bench.copied_pred(A, 10, 9)])
+        tab.finalize()
+        c2.append(tab.info())
+    tab.destroy()
+    del ev, cols
+    torch.cuda.empty_cache()
+    cdf5 = E.zipf_cdf(bench.C5_KEYS, bench.C5_ZIPF)
+    ev = E.gen_file(0xC5, 0, bench.C5_KEYS, H.to_device(cdf5), 0, NC)
+    cols = [ev[k] for k in bench.C5_NAMES]
+    tab = E.Table(bench.C5_WIDTHS, bench.c5_aggs(A), bench.C5_CAP)
+    c5 = []
+    for _ in range(5):
+        tab.reset()
+        tab.update(cols, [0, 1, 2, 3], NC, 0)
+        tab.finalize()
+        c5.append(tab.info())
+    tab.destroy()
+    del ev, cols
+    torch.cuda.empty_cache()
+    print("c2", [(i["loaders"], i["miss_permille"]) for i in c2], "c5", [(i["loaders"], i["miss_permille"]) for i in c5])
+    assert all(i["form"] == A.GB_CACHED for i in c2 + c5)
+    assert all(i["loaders"] == 8 for i in c2), c2
+    assert all(300 < i["miss_permille"] < 370 for i in c2), c2
+    assert all(i["loaders"] == 7 for i in c5), c5
+    assert all(i["miss_permille"] > 390 for i in c5), c5

@@ -350,3 +350,82 @@ def test_nan_sort_hand_derived_vectors(igx, torch):
             cols = [(H.to_device(np.array(v, dt)), d) for v, d in keys]
             got = H.host(E.sort_perm(cols, n, valid=dv)).astype(np.int64)
             assert list(got) == want, (keys, valid, dt)
+
+
+def test_device_planned_sort_matches_host_planned(oracle, E, H, torch, monkeypatch):
+    """The device-planned LSD passes (IGX_SORT_DEVPLAN=1, k_lsd_*: each pass decides on the device
+    whether its digit varies, one launch per pass, tiles chained by tagged counts) against the
+    default host-planned passes and the Go SliceStable restatement: 1..8 composed words, ties,
+    nil rows, several tiles, and a selection vector whose length stays on the device (both
+    paths: the host plan reads the count back with its AND/OR words)."""
+    rng = np.random.default_rng(11)
+    for trial, n in enumerate([1, 2, 3, 4095, 4096, 4097, 70_000, 300_001]):
+        nk = int(rng.integers(1, 4))
+        kinds = rng.choice(["int8", "int64", "uint16", "uint32", "string"], nk)
+        keys_d, keys_o = [], []
+        for kd in kinds:
+            desc = bool(rng.random() < 0.5)
+            if kd == "string":
+                a = np.zeros((n, 12), np.uint8)
+                a[:, 0] = rng.integers(97, 103, n)
+                a[:, 5] = rng.integers(0, 3, n) * 40
+            else:
+                lo = -50 if kd.startswith("int") else 0
+                a = rng.integers(lo, 50, n).astype(kd)
+            keys_d.append((H.to_device(a), desc))
+            keys_o.append((a, kd, desc))
+        valid = (rng.random(n) < 0.9).astype(np.uint8) if trial % 2 else None
+        vd = None if valid is None else H.to_device(valid)
+        monkeypatch.setenv("IGX_SORT_DEVPLAN", "1")
+        got = H.host(E.sort_perm(keys_d, n, valid=vd))
+        monkeypatch.delenv("IGX_SORT_DEVPLAN")
+        host = H.host(E.sort_perm(keys_d, n, valid=vd))
+        ref = oracle.go_sort_entries(keys_o, n, valid=valid)
+        assert np.array_equal(host, ref), (trial, kinds)
+        assert np.array_equal(got, ref), (trial, kinds)
+        # a selection of m rows (every third row, reversed) of capacity n, its count on the device
+        sel = np.arange(n, dtype=np.uint32)[::-3].copy()
+        m = len(sel)
+        cap = torch.full((n,), 0xFFFF, dtype=torch.int32, device="cuda").view(torch.uint32)
+        cap[:m] = H.to_device(sel)
+        cnt = torch.tensor([m], dtype=torch.int64, device="cuda").view(torch.uint64)
+        sub = [(a[sel], kd, d) for a, kd, d in keys_o]
+        want = sel[oracle.go_sort_entries(sub, m, valid=None if valid is None else valid[sel]).astype(np.int64)]
+        for devplan in (False, True):
+            if devplan:
+                monkeypatch.setenv("IGX_SORT_DEVPLAN", "1")
+            out = H.host(E.sort_perm(keys_d, n, valid=vd, rowmap=cap, d_count=cnt))[:m]
+            monkeypatch.delenv("IGX_SORT_DEVPLAN", raising=False)
+            assert np.array_equal(out, want), (trial, kinds, devplan)
+
+
+@pytest.mark.parametrize("devplan", [False, True])
+def test_filter_then_sort_pending_count(oracle, E, H, igx, torch, monkeypatch, devplan):
+    """C1's step as the bench runs it: FilterEntries leaves its survivor count on the device and
+    SortEntries sorts that pending view (igx_sort_perm_dn: the host plan reads the count back
+    with its AND/OR words -- one round trip for the whole step; IGX_SORT_DEVPLAN=1: none); the
+    view's length is read only afterwards.  Same rows, same order as the oracle's FilterEntries
+    + SortEntries."""
+    if devplan:
+        monkeypatch.setenv("IGX_SORT_DEVPLAN", "1")
+    n = 1_000_000
+    ccdf = oracle.zipf_cdf(64, 1.0)
+    ev_h = oracle.gen_open(0xC1, ccdf, 0, n)
+    cols = igx.columns.Columns([("pid", "uint32"), ("uid", "uint32"), ("mntns", "uint64"),
+                                ("comm", "string", 16), ("ret", "int64"), ("fd", "int64"),
+                                ("err", "int64"), ("path", "uint32")])
+    batch = igx.columns.EventBatch(cols, {k: H.to_device(v) for k, v in ev_h.items()})
+    for filters, sort_by in ((["err:0", "pid:>=1000"], ["comm", "-pid"]), (["uid:0"], ["-comm", "pid", "-fd"]),
+                             (["pid:<0"], ["comm"])):
+        out = igx.filter.FilterEntries(cols, batch, filters)
+        assert out.pending() is not None
+        srt = igx.sort.SortEntries(cols, out, sort_by)
+        assert srt.pending() is not None              # the view's length is still on the device
+        ocols = {c: oracle.OCol(c, t, w) for c, t, w in (("err", "int64", 8), ("pid", "uint32", 4),
+                                                           ("uid", "uint32", 4))}
+        sel = oracle.filter_entries(ocols, {k: ev_h[k] for k in ("err", "pid", "uid")}, None, filters)
+        kinds = {"comm": "string", "pid": "uint32", "fd": "int64"}
+        keys = [(ev_h[s.lstrip("-")][sel], kinds[s.lstrip("-")], s.startswith("-")) for s in sort_by]
+        want = sel[oracle.go_sort_entries(keys, len(sel)).astype(np.int64)]
+        assert srt.n == len(sel)
+        assert np.array_equal(H.host(srt.sel).astype(np.int64), want.astype(np.int64)), filters
