@@ -344,8 +344,10 @@ int igx_groupby_info(igx_table *t, igx_groupby_info_t *out);
  * would have returned (IGX_ENOSPC) come back from igx_groupby_wait, or from the first
  * igx_groupby_reset / igx_groupby_finalize that finds the read-back landed (a reset never
  * waits for the device), or, when the next interval's igx_groupby_finalize_async collects it,
- * from that call (which still issues its own interval; the error text names the failed
- * finalize) -- igx_groupby_wait only ever reports the last finalize's own status.  The read-back is written by the kernel that counts the groups into
+ * from that call, which then does NOT issue its own interval (the error text names the failed
+ * finalize; calling it again finalizes this interval: a non-zero return always means "not
+ * finalized") -- igx_groupby_wait only ever reports the last finalize's own status.  The
+ * read-back is written by the kernel that counts the groups into
  * the table's coherent pinned buffer, followed by a sequence number the host polls (no copy
  * and no event on the stream); igx_groupby_wait polls it, and fails with IGX_EIO if the
  * stream drains without it.  Asynchronous. */

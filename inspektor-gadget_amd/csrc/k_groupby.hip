@@ -2671,22 +2671,23 @@ extern "C" int igx_groupby_finalize(igx_table *t, igx_table_view *view) {
 extern "C" int igx_groupby_finalize_async(igx_table *t, igx_table_view *view) {
     if (!t) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    // the previous interval's read-back (it precedes this interval) is collected first; a
-    // failure of that interval comes back from this call -- after this interval is issued,
-    // so the caller's pipeline stays intact -- and igx_groupby_wait reports this one's only
+    // the previous interval's read-back (it precedes this interval) is collected first.  A
+    // failure of that interval is returned by this call WITHOUT issuing this interval (the view
+    // is left untouched), once: a non-zero return always means "not finalized", and calling
+    // again issues the interval.  igx_groupby_wait reports an interval's own status only.
     (void)fin_collect(t, nullptr);
-    const int earlier = t->fin_status;
-    const uint64_t earlier_seq = t->fin_status_seq;
-    t->fin_status = IGX_OK;
+    if (const int earlier = t->fin_status) {
+        const uint64_t earlier_seq = t->fin_status_seq;
+        t->fin_status = IGX_OK;
+        const std::string why = igx_last_error(ctx);   // the collected interval's message
+        return igx_fail(ctx, earlier, "groupby: the previous interval (finalize %llu) failed: %s; this interval "
+                                      "was not finalized",
+                        (unsigned long long)earlier_seq, why.c_str());
+    }
     const int rc = fin_launch(t);
     if (rc) return rc;
     t->fin_pending = true;
     fin_view(t, view, 0);
-    if (earlier) {
-        const std::string why = igx_last_error(ctx);   // the collected interval's message
-        return igx_fail(ctx, earlier, "groupby: the previous interval (finalize %llu) failed: %s",
-                        (unsigned long long)earlier_seq, why.c_str());
-    }
     return IGX_OK;
 }
 

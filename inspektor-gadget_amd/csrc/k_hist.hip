@@ -75,9 +75,22 @@ __device__ __forceinline__ uint64_t divide(uint64_t v, uint64_t d) {
 
 template <int DIV>
 __device__ __forceinline__ uint32_t slot_of(int64_t d, uint64_t divisor, uint32_t nslots) {
-    const uint64_t v = divide<DIV>((uint64_t)d, divisor);
-    const uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
-    return min(slot, nslots - 1);
+    if constexpr (DIV == 1000 || DIV == 1000000) {
+        // log2l(v / D) without the 64-bit division (a 128-bit multiply-high per row): with
+        // L = floor(log2 v) and 2^(C-1) <= D < 2^C, floor(log2(floor(v / D))) is L - C + 1 when
+        // D << (L - C + 1) <= v and L - C otherwise -- exact, since floor(v / D) >= 2^k iff
+        // v >= D * 2^k (D * 2^k is an integer).  v < D: slot 0 (log2l(0) == 0).
+        constexpr uint32_t C = DIV == 1000 ? 10u : 20u;
+        const uint64_t v = (uint64_t)d;
+        if (v < (uint64_t)DIV) return 0u;
+        const uint32_t k1 = 63u - (uint32_t)__clzll(v) - C + 1u;
+        const uint32_t k = ((uint64_t)DIV << k1) <= v ? k1 : k1 - 1u;
+        return min(k, nslots - 1);
+    } else {
+        const uint64_t v = divide<DIV>((uint64_t)d, divisor);
+        const uint32_t slot = v ? 63u - (uint32_t)__clzll(v) : 0u;
+        return min(slot, nslots - 1);
+    }
 }
 
 // Slot window start from this workgroup's sample: wcnt[slot] holds the sampled rows per slot;

@@ -429,3 +429,31 @@ def test_filter_then_sort_pending_count(oracle, E, H, igx, torch, monkeypatch, d
         want = sel[oracle.go_sort_entries(keys, len(sel)).astype(np.int64)]
         assert srt.n == len(sel)
         assert np.array_equal(H.host(srt.sel).astype(np.int64), want.astype(np.int64)), filters
+
+
+@pytest.mark.parametrize("divisor", [1000, 1000000, 7])
+def test_hist_slot_boundaries(oracle, E, H, torch, divisor):
+    """log2l(delta / divisor) at every boundary D * 2^k - 1, D * 2^k, D * 2^k + 1 (and powers of
+    two, zero, negatives): the division-free slot of k_hist (divisors 1000 / 1e6) and the
+    generic one agree with biolatency.bpf.c:133-141 / bits.bpf.h:8-29 as the oracle restates it."""
+    vals = [0, 1, -1, -5, (1 << 63) - 1]
+    for k in range(0, 62):
+        for base in (divisor << k, 1 << k):
+            for e in (-1, 0, 1):
+                v = base + e
+                if 0 <= v < (1 << 63):
+                    vals.append(v)
+    rng = np.random.default_rng(5)
+    vals += list(rng.integers(0, 1 << 62, 5000))
+    vals += [0] * (-len(vals) % 8192 + 8192 * 4)   # whole 8192-row chunks: the vector path too
+    delta = np.array(vals, dtype=np.int64)
+    n = len(delta)
+    d = H.to_device(delta)
+    ref = oracle.hist_log2(None, None, delta, [], 1, divisor=divisor)
+    assert ref.sum() == (delta >= 0).sum()
+    got = H.host(E.hist_log2(None, None, d, [], 1, divisor=divisor))            # scalar loads
+    assert np.array_equal(got, ref)
+    devc = H.to_device(np.full(n, 7, np.uint32))
+    contc = H.to_device(np.zeros(n, np.uint32))
+    got = H.host(E.hist_log2(devc, contc, d, [7], 1, divisor=divisor))          # 16-B loads
+    assert np.array_equal(got, ref)
