@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 METRIC = "events aggregated/sec (filter+group-by+top-K) at 1/2/4/8 MI355X; % HBM peak"   # BASELINE.json
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 EV_BYTES = 71                  # saddr16 daddr16 mntns8 pid4 comm16 lport2 dport2 family2 size4 dir1
 GROUP_BYTES = 90               # key 66 + sent 8 + recv 8 + first_idx 8
 TCP_NAMES = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
