@@ -274,6 +274,25 @@ def gather_checks(ctx, obj):
     return out
 
 
+def merge_rank_topk(O, recs, K):
+    """The oracle's global top-K from every rank's top-K (rank-disjoint key universes): the
+    union ordered by SortStats(["-sent","-recv"]) with the global first index as the
+    pre-sort position (Go SliceStable via the oracle).  Returns (sent, recv, first) of the first
+    K.  tests/test_bench_check.py checks it against the oracle run over the union's events."""
+    S = np.concatenate([r["sent"] for r in recs])
+    R = np.concatenate([r["recv"] for r in recs])
+    F = np.concatenate([r["first"] for r in recs])
+    order = np.argsort(F, kind="stable")              # pre-sort position = global first index
+    perm = O.go_sort_entries([(S[order], "uint64", True), (R[order], "uint64", True)], len(F))
+    sel = order[perm[:K].astype(np.int64)]
+    return S[sel], R[sel], F[sel]
+
+
+def sum_rank_hists(refs):
+    """Every rank's oracle histogram summed with u32 wrap, like the device's all-reduce."""
+    return np.sum([r.astype(np.uint64) for r in refs], axis=0).astype(np.uint32)
+
+
 def check_c2(a, ctx, tab, cand, cdf_h, Gn):
     """C2's last timed interval vs or_top_tcp_mt on the same stream: this rank's group count
     and whole-table checksum (key fields, sent, recv, first index of every group), and the
@@ -292,14 +311,9 @@ def check_c2(a, ctx, tab, cand, cdf_h, Gn):
                                "sent": sent, "recv": recv, "first": first})
     if rank != 0:
         return None
-    S = np.concatenate([r["sent"] for r in recs])
-    R = np.concatenate([r["recv"] for r in recs])
-    F = np.concatenate([r["first"] for r in recs])
-    order = np.argsort(F, kind="stable")              # pre-sort position = global first index
-    perm = O.go_sort_entries([(S[order], "uint64", True), (R[order], "uint64", True)], len(F))
-    sel = order[perm[:K].astype(np.int64)]
+    S, R, F = merge_rank_topk(O, recs, K)
     c = H.host(cand)
-    top_ok = topk_equal(c, (72, 80), 88, F[sel], (S[sel], R[sel]))
+    top_ok = topk_equal(c, (72, 80), 88, F, (S, R))
     groups_ok = all(r["groups"] == r["oracle_groups"] for r in recs)
     cs_ok = all(r["checksum_equal"] for r in recs)
     return {"bit_exact": bool(groups_ok and cs_ok and top_ok), "groups_equal": bool(groups_ok),
@@ -514,7 +528,7 @@ def run_c3(a, ctx):
         del hh
         refs = gather_checks(ctx, ref)
         if rank == 0:
-            tot = np.sum([r.astype(np.uint64) for r in refs], axis=0).astype(np.uint32)   # u32 wrap like the device
+            tot = sum_rank_hists(refs)
             ok = bool(np.array_equal(H.host(hist), tot))
             out["check"] = {"bit_exact": ok, "what": "last timed step's whole u32[4096][27] histogram vs the sum "
                                                      f"of {world} rank(s)' oracle histograms"}

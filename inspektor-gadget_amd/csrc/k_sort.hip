@@ -34,8 +34,12 @@ constexpr int TILE = TB * IPT;   // 4096 rows per tile
 // The radix passes' histogram and scatter kernels run a tile with 1024 threads (4 rows each):
 // at ~1M rows a pass has about one tile per CU, and a 256-thread block working through 16
 // rows per thread one barrier step at a time left the pass latency-bound (~30 us).
-constexpr int STB = 1024;
-constexpr int SIPT = TILE / STB;
+#ifndef IGX_RADIX_STB
+#define IGX_RADIX_STB 1024
+#endif
+constexpr int STB = IGX_RADIX_STB;
+constexpr int SIPT = 4;
+constexpr int RTILE = STB * SIPT;   // rows per radix-pass tile
 constexpr int MAXW = 80;          // composed words (keys + pos + nil; wider keys: ENOTSUP)
 constexpr int NSK = 32;           // sort keys
 
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(STB) void k_radix_hist(const uint32_t *__restrict__
     const uint32_t t = threadIdx.x, wave = t >> 6;
     for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t base = (uint64_t)blockIdx.x * RTILE;
     uint32_t d[SIPT];
 #pragma unroll
     for (int j = 0; j < SIPT; ++j) {
@@ -382,10 +386,11 @@ constexpr uint32_t SCAN_FREE_TILES = 512;
 // flight per thread; the quarters' sums meet in LDS and the digit totals are scanned across
 // the first 256 threads -- the three scan kernels a pass would otherwise need.  Called by the
 // whole block; threads 0..255 get digit t's base, the others 0.  tmp: 4 + 2 x 1024 words.
+constexpr uint32_t NPART = STB / 256;   // 256-thread parts of a radix block
 __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t *tmp) {
     const uint32_t t = threadIdx.x & 255u, part = threadIdx.x >> 8, lane = t & 63, wave = t >> 6;
     const uint32_t me = blockIdx.x;
-    const uint32_t q0 = (uint32_t)((uint64_t)nb * part / 4), q1 = (uint32_t)((uint64_t)nb * (part + 1) / 4);
+    const uint32_t q0 = (uint32_t)((uint64_t)nb * part / NPART), q1 = (uint32_t)((uint64_t)nb * (part + 1) / NPART);
     uint32_t pre = 0, tot = 0;
     uint32_t q = q0;
     for (; q + 16 <= q1; q += 16) {
@@ -403,14 +408,19 @@ __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__
         tot += v;
         if (q < me) pre += v;
     }
-    uint32_t *spre = tmp + 4, *stot = tmp + 4 + 1024;
+    uint32_t *spre = tmp + 4, *stot = tmp + 4 + STB;
     spre[threadIdx.x] = pre;
     stot[threadIdx.x] = tot;
     __syncthreads();
     const bool mine = threadIdx.x < 256;
     if (mine) {
-        pre = spre[t] + spre[256 + t] + spre[512 + t] + spre[768 + t];
-        tot = stot[t] + stot[256 + t] + stot[512 + t] + stot[768 + t];
+        pre = 0;
+        tot = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NPART; ++q) {
+            pre += spre[256 * q + t];
+            tot += stot[256 * q + t];
+        }
     }
     uint32_t inc = mine ? tot : 0u;
 #pragma unroll
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(STB) void k_radix_scatter(ScatterArgs a) {
     }
     for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+    const uint64_t tbase = (uint64_t)blockIdx.x * RTILE;
     const uint32_t *dw = a.in[a.dword];
     for (int j = 0; j < SIPT; ++j) {
         const uint64_t i = tbase + (uint64_t)j * STB + t;
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(STB) void k_radix_scatter_pf(ScatterArgs a) {
     }
     for (uint32_t i = t; i < (STB / 64) * 256; i += STB) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+    const uint64_t tbase = (uint64_t)blockIdx.x * RTILE;
     uint32_t cw[SIPT][NLMAX], cp[SIPT];
 #pragma unroll
     for (int j = 0; j < SIPT; ++j) {
@@ -603,7 +613,7 @@ __global__ __launch_bounds__(STB) void k_lsd_h0(const uint32_t *__restrict__ W, 
                                                 uint64_t nmax, const uint64_t *__restrict__ d_n, LsdCtl *ctl) {
     __shared__ uint32_t h[256];
     const uint32_t n = lsd_n(nmax, d_n);
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t base = (uint64_t)blockIdx.x * RTILE;
     if (base >= n) return;
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
@@ -632,9 +642,9 @@ struct LsdArgs {
 template <int NLMAX>
 __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
     __shared__ uint32_t wc[SIPT][STB / 64][256];   // counts, then exclusive offsets inside each digit
-    __shared__ uint32_t gb[256], toff[256], base[256], qsum[4][256], hn[256];
-    __shared__ uint32_t stage[TILE];
-    __shared__ uint8_t sdig[TILE];
+    __shared__ uint32_t gb[256], toff[256], base[256], qsum[NPART < 4 ? 4 : NPART][256], hn[256];
+    __shared__ uint32_t stage[RTILE];
+    __shared__ uint8_t sdig[RTILE];
     __shared__ uint32_t tile_s, flags;
     const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t n = lsd_n(a.nmax, a.d_n);
@@ -657,7 +667,7 @@ __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
     const uint32_t cur = a.ctl->cur;
     if (flags || n < 2) {
         // inactive: only the next digit's histogram (over this block's rows of the unchanged buffer)
-        const uint64_t tb = (uint64_t)blockIdx.x * TILE;
+        const uint64_t tb = (uint64_t)blockIdx.x * RTILE;
         if (!has_next || tb >= n || n < 2) return;
         const uint32_t *col = a.W[cur] + (uint64_t)wn * a.stride;
 #pragma unroll
@@ -689,10 +699,10 @@ __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
     }
     __syncthreads();   // qsum is rewritten by the predecessor sums below
     const uint32_t tile = tile_s;
-    const uint32_t ntiles = (n + TILE - 1) / TILE;
+    const uint32_t ntiles = (n + RTILE - 1) / RTILE;
     if (tile >= ntiles) return;
     const uint32_t nl = w + 1;   // every word up to this one is carried
-    const uint64_t tbase = (uint64_t)tile * TILE;
+    const uint64_t tbase = (uint64_t)tile * RTILE;
     uint32_t cw[SIPT][NLMAX], cp[SIPT], dg[SIPT], rk[SIPT];
 #pragma unroll
     for (int j = 0; j < SIPT; ++j) {
@@ -740,7 +750,7 @@ __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
     // the counts of the tiles before this one: four quarters of 256 threads, one digit each
     {
         const uint32_t d = t & 255u, q = t >> 8;
-        const uint32_t q0 = tile * q / 4, q1 = tile * (q + 1) / 4;
+        const uint32_t q0 = tile * q / NPART, q1 = tile * (q + 1) / NPART;
         uint32_t sum = 0;
         for (uint32_t j = q0; j < q1; j += 8) {   // 8 polls in flight per thread
             uint64_t v[8];
@@ -777,7 +787,10 @@ __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
             const uint32_t y = __shfl_up(inc, d);
             if ((int)lane >= d) inc += y;
         }
-        base[t] = gb[t] + qsum[0][t] + qsum[1][t] + qsum[2][t] + qsum[3][t];
+        uint32_t pre = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NPART; ++q) pre += qsum[q][t];
+        base[t] = gb[t] + pre;
         gb[t] = inc - c;   // wave-local exclusive start (gb is free now)
         if (lane == 63) hn[wave] = inc;   // wave totals (hn is free now)
     }
@@ -795,7 +808,7 @@ __global__ __launch_bounds__(STB) void k_lsd_pass(LsdArgs a) {
         lp[j] = toff[dg[j]] + wc[j][wave][dg[j]] + rk[j];
         if (tbase + (uint64_t)j * STB + t < n) sdig[lp[j]] = (uint8_t)dg[j];
     }
-    const uint32_t tn = min<uint32_t>(TILE, n - (uint32_t)tbase);
+    const uint32_t tn = min<uint32_t>(RTILE, n - (uint32_t)tbase);
     for (uint32_t l = 0; l <= nl; ++l) {   // l == nl: the payload
         __syncthreads();
 #pragma unroll
@@ -1421,7 +1434,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const uint64_t stride = igx_align(nrows, 64);
     ca.stride = stride;
 
-    const uint32_t nblocks = (uint32_t)((nrows + TILE - 1) / TILE);
+    const uint32_t nblocks = (uint32_t)((nrows + RTILE - 1) / RTILE);
     const size_t words_b = igx_align((size_t)KW * stride * 4, 256);
     const size_t pay_b = igx_align(stride * 4, 256);
     const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
@@ -1641,7 +1654,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         nrows = std::min<uint64_t>(nrows, dn);
         if (nrows == 0) return IGX_OK;
     }
-    const uint32_t pblocks = (uint32_t)((nrows + TILE - 1) / TILE);
+    const uint32_t pblocks = (uint32_t)((nrows + RTILE - 1) / RTILE);
     // digit plan: word w (0 = most significant), byte b (0 = least significant in word)
     std::vector<int> live_word(KW, 0);
     for (uint32_t w = 0; w < KW; ++w) live_word[w] = (hres[2 * w] ^ hres[2 * w + 1]) != 0;
