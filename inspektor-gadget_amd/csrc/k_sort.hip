@@ -43,21 +43,6 @@ constexpr int RTILE = STB * SIPT;   // rows per radix-pass tile
 constexpr int MAXW = 80;          // composed words (keys + pos + nil; wider keys: ENOTSUP)
 constexpr int NSK = 32;           // sort keys
 
-struct ComposeArgs {
-    const uint8_t *ptr[NSK];
-    uint32_t width[NSK], kind[NSK], desc[NSK], words[NSK], rstride[NSK], direct[NSK];   // direct: read at i, not rowmap[i]
-    uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
-    uint32_t reverse;     // pos_words == 0: slot i holds row n-1-i (the position order is descending)
-    const uint64_t *pos;
-    const uint8_t *valid;
-    const uint32_t *rowmap;
-    const uint64_t *d_n;  // nullable: the row count on the device (n is then its upper bound)
-    uint64_t n, stride;   // stride = words array pitch (elements)
-    uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN (k_andor_final
-                          // moves it into res and clears it: the word is the context's, zero
-                          // between sorts)
-};
-
 __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, uint32_t j) {
     if (4 * j + 4 <= width && (reinterpret_cast<uintptr_t>(p) & 3) == 0)   // a whole aligned dword
         return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(p + 4 * j));
@@ -69,6 +54,255 @@ __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, ui
     }
     return v;
 }
+
+// ---- string dictionaries -------------------------------------------------------------
+// A multi-word string key costs one radix pass per live byte (C1's 16-byte `comm`: 12 of its
+// 16 passes).  When the key has few distinct values, the sort replaces it by its rank among
+// them: equal strings get equal ranks and the ranks keep the strings' byte order, so the
+// stable LSD passes over the rank produce exactly the order of the passes over the bytes --
+// with one or two live digits instead of a dozen.  k_dict_build collects the distinct values
+// (an open-addressed table of {tag, index} slots; the values themselves in claim order),
+// k_dict_rank sorts them in one workgroup's LDS (bitonic, over indices) and k_compose looks
+// every row's rank up.  More distinct values than the dictionary holds void it (ctl[1]); the
+// host then composes the raw bytes (one more read-back, launch_sort_perm).
+constexpr int DICT_W = 8;                // key words a dictionary takes (strings of <= 32 bytes)
+constexpr uint32_t DICT_MAXD = 4096;     // distinct values (power of two)
+constexpr uint32_t DICT_LDS_WORDS = 16384;   // k_dict_rank: distinct values x words in LDS
+constexpr int DICT_MAXK = 4;             // dictionary keys per sort
+constexpr uint64_t DICT_MIN_ROWS = 1u << 16;
+
+struct DictRef {
+    uint32_t *slot;     // 2 x (mask + 1): {tag (0 empty, 1 being written, else hash | 2), index}
+    uint32_t *keys;     // cap x nw: the distinct values' words, in claim order
+    uint32_t *rankof;   // cap: rank of value i among the distinct values
+    uint32_t *ctl;      // [0] distinct values claimed, [1] void (over capacity)
+    uint32_t mask, cap, nw;
+};
+
+struct DictBuildArgs {
+    DictRef d;
+    const uint8_t *ptr;
+    uint32_t width, rstride;
+    const uint32_t *rowmap;
+    const uint8_t *valid;
+    const uint64_t *d_n;
+    uint64_t n;
+};
+
+__device__ __forceinline__ uint32_t dict_hash(const uint32_t (&k)[DICT_W], uint32_t nw) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (int j = 0; j < DICT_W; ++j)
+        if ((uint32_t)j < nw) h = (h ^ k[j]) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    h *= 0xC4CEB9FE1A85EC53ull;
+    h ^= h >> 29;
+    return (uint32_t)h;
+}
+
+__device__ __forceinline__ bool dict_eq(const uint32_t *v, const uint32_t (&k)[DICT_W], uint32_t nw) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < DICT_W; ++j)
+        if ((uint32_t)j < nw) diff |= v[j] ^ k[j];
+    return diff == 0;
+}
+
+// Insert a value into the global table (the value's hash h).  One probe per iteration: a lane
+// that finds its slot being written looks again next iteration, so a claimer of the same wave
+// (which publishes within its own iteration) is never waited for inside a branch.
+__device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint32_t h) {
+    const uint32_t tg = h | 2u;
+    uint32_t s = h & d.mask;
+    for (uint32_t probes = 0, spins = 0; probes <= d.mask;) {
+        const uint32_t t = __hip_atomic_load(&d.slot[2 * s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0u) {
+            if (atomicCAS(&d.slot[2 * s], 0u, 1u) == 0u) {
+                const uint32_t idx = atomicAdd(&d.ctl[0], 1u);
+                if (idx >= d.cap) {   // over capacity: the dictionary is void (the slot stays busy)
+                    atomicOr(&d.ctl[1], 1u);
+                    return;
+                }
+#pragma unroll
+                for (int j = 0; j < DICT_W; ++j)
+                    if ((uint32_t)j < d.nw) d.keys[(uint64_t)idx * d.nw + j] = k[j];
+                d.slot[2 * s + 1] = idx;
+                __hip_atomic_store(&d.slot[2 * s], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            continue;   // lost the claim: read the slot again
+        }
+        if (t == 1u) {   // being written
+            if (__hip_atomic_load(&d.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+            if (++spins > (1u << 20)) { atomicOr(&d.ctl[1], 2u); return; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (t == tg) {
+            const uint32_t idx = d.slot[2 * s + 1];
+            if (dict_eq(d.keys + (uint64_t)idx * d.nw, k, d.nw)) return;
+        }
+        s = (s + 1) & d.mask;
+        ++probes;
+    }
+    atomicOr(&d.ctl[1], 2u);   // no free slot (cannot happen: at most half the slots are claimed)
+}
+
+// Each workgroup first collects the distinct values of its DB_ROWS rows in LDS and then
+// inserts only those into the global table: a few distinct values over a million rows would
+// otherwise send every row's (L1-bypassing) probe to the same few L2 lines (measured: 0.91 ms
+// for C1's 0.87M rows and 64 names).  A block with more than DL_CAP distinct values sends the
+// rest straight to the global table.
+constexpr uint32_t DB_T = 1024, DB_RPT = 4, DB_ROWS = DB_T * DB_RPT;
+constexpr uint32_t DL_SLOTS = 2048, DL_CAP = 1024, DL_NONE = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
+    __shared__ uint32_t ltag[DL_SLOTS];   // 0 empty, 1 being written, else hash | 2
+    __shared__ uint32_t lidx[DL_SLOTS];   // the value's local index, DL_NONE: it went global
+    __shared__ uint32_t lval[DL_CAP * DICT_W];
+    __shared__ uint32_t lhash[DL_CAP];
+    __shared__ uint32_t lcount;
+    const DictRef &d = a.d;
+    for (uint32_t t = threadIdx.x; t < DL_SLOTS; t += DB_T) ltag[t] = 0;
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    const uint64_t n = a.d_n ? min(a.n, *a.d_n) : a.n;
+    const uint64_t base = (uint64_t)blockIdx.x * DB_ROWS + threadIdx.x;
+    // every row's words first (all loads in flight together), then the inserts
+    uint32_t k[DB_RPT][DICT_W];
+    bool live[DB_RPT];
+#pragma unroll
+    for (int r = 0; r < (int)DB_RPT; ++r) {
+        const uint64_t i = base + (uint64_t)r * DB_T;
+        live[r] = i < n;
+        const uint64_t src = live[r] ? (a.rowmap ? a.rowmap[i] : i) : 0;
+        if (live[r] && a.valid) live[r] = a.valid[src] != 0;   // nil rows compose zeros, not a rank
+        const uint8_t *p = a.ptr + src * a.rstride;
+#pragma unroll
+        for (int j = 0; j < DICT_W; ++j) k[r][j] = live[r] && (uint32_t)j < d.nw ? be_word(p, a.width, j) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < (int)DB_RPT; ++r) {
+        if (!live[r]) continue;
+        const uint32_t h = dict_hash(k[r], d.nw), tg = h | 2u;
+        uint32_t s = h & (DL_SLOTS - 1);
+        bool global = false;
+        for (uint32_t probes = 0, spins = 0; probes < DL_SLOTS;) {
+            const uint32_t t = __hip_atomic_load(&ltag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == 0u) {
+                if (atomicCAS(&ltag[s], 0u, 1u) == 0u) {
+                    const uint32_t li = atomicAdd(&lcount, 1u);
+                    if (li < DL_CAP) {
+#pragma unroll
+                        for (int j = 0; j < DICT_W; ++j)
+                            if ((uint32_t)j < d.nw) lval[li * d.nw + j] = k[r][j];
+                        lhash[li] = h;
+                        lidx[s] = li;
+                    } else {
+                        lidx[s] = DL_NONE;   // this value (and any sharing its hash) goes global
+                        global = true;
+                    }
+                    __hip_atomic_store(&ltag[s], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                continue;
+            }
+            if (t == 1u) {
+                if (++spins > (1u << 22)) { atomicOr(&d.ctl[1], 2u); break; }
+                continue;
+            }
+            if (t == tg) {
+                const uint32_t li = lidx[s];
+                if (li == DL_NONE) { global = true; break; }
+                if (dict_eq(lval + li * d.nw, k[r], d.nw)) break;
+            }
+            s = (s + 1) & (DL_SLOTS - 1);
+            ++probes;
+        }
+        if (global) dict_insert(d, k[r], h);
+    }
+    __syncthreads();
+    const uint32_t nloc = min(lcount, DL_CAP);
+    for (uint32_t li = threadIdx.x; li < nloc; li += DB_T) {
+        uint32_t v[DICT_W];
+#pragma unroll
+        for (int j = 0; j < DICT_W; ++j) v[j] = (uint32_t)j < d.nw ? lval[li * d.nw + j] : 0u;
+        dict_insert(d, v, lhash[li]);
+    }
+}
+
+// One workgroup: the distinct values into LDS, a bitonic sort of their indices (the values are
+// distinct, so no tie order to keep), rankof[index] = position.
+__global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
+    extern __shared__ uint32_t dl[];
+    if (d.ctl[1]) return;   // void: the host composes the raw bytes
+    const uint32_t D = min(d.ctl[0], d.cap), nw = d.nw;
+    uint32_t N = 2;
+    while (N < D) N <<= 1;
+    uint32_t *kv = dl, *ix = dl + (size_t)d.cap * nw;
+    for (uint32_t t = threadIdx.x; t < D * nw; t += 1024) kv[t] = d.keys[t];
+    for (uint32_t t = threadIdx.x; t < N; t += 1024) ix[t] = t;
+    __syncthreads();
+    // greater(a, b): pad indices (>= D) sort last
+    auto greater = [&](uint32_t a, uint32_t b) -> bool {
+        if (a >= D || b >= D) return a >= D && (b < D || a > b);
+        const uint32_t *x = kv + (size_t)a * nw, *y = kv + (size_t)b * nw;
+        for (uint32_t j = 0; j < nw; ++j)
+            if (x[j] != y[j]) return x[j] > y[j];
+        return false;
+    };
+    for (uint32_t k = 2; k <= N; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < N; t += 1024) {
+                const uint32_t u = t ^ j;
+                if (u > t) {
+                    const uint32_t a = ix[t], b = ix[u];
+                    if (greater(a, b) == ((t & k) == 0)) {
+                        ix[t] = b;
+                        ix[u] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = threadIdx.x; t < D; t += 1024) d.rankof[ix[t]] = t;
+}
+
+// the rank of a row's value (k_compose; the value is in the dictionary unless it is void)
+__device__ __forceinline__ uint32_t dict_rank(const DictRef &d, const uint8_t *p, uint32_t width) {
+    uint32_t k[DICT_W];
+#pragma unroll
+    for (int j = 0; j < DICT_W; ++j) k[j] = (uint32_t)j < d.nw ? be_word(p, width, j) : 0u;
+    const uint32_t h = dict_hash(k, d.nw), tg = h | 2u;
+    uint32_t s = h & d.mask;
+    for (uint32_t probes = 0; probes <= d.mask; ++probes, s = (s + 1) & d.mask) {
+        const uint32_t t = d.slot[2 * s];
+        if (t == 0u) break;
+        if (t == tg) {
+            const uint32_t idx = d.slot[2 * s + 1];
+            if (idx < d.cap && dict_eq(d.keys + (uint64_t)idx * d.nw, k, d.nw)) return d.rankof[idx];
+        }
+    }
+    return 0u;   // only when the dictionary is void (the host then discards this compose)
+}
+
+struct ComposeArgs {
+    const uint8_t *ptr[NSK];
+    uint32_t width[NSK], kind[NSK], desc[NSK], words[NSK], rstride[NSK], direct[NSK];   // direct: read at i, not rowmap[i]
+    uint32_t dict[NSK];                  // 0, or 1 + the key's dictionary (words[k] is then 1: the rank)
+    DictRef dref[DICT_MAXK];
+    uint32_t nkeys, has_nil, pos_words, pos_not, pos_stride;   // pos_stride in bytes
+    uint32_t reverse;     // pos_words == 0: slot i holds row n-1-i (the position order is descending)
+    const uint64_t *pos;
+    const uint8_t *valid;
+    const uint32_t *rowmap;
+    const uint64_t *d_n;  // nullable: the row count on the device (n is then its upper bound)
+    uint64_t n, stride;   // stride = words array pitch (elements)
+    uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN (k_andor_final
+                          // moves it into res and clears it: the word is the context's, zero
+                          // between sorts)
+};
 
 __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
                                                 uint32_t *__restrict__ payload) {
@@ -89,7 +323,9 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
         }
         const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
         const uint8_t *p = a.ptr[k] + (a.direct[k] ? r : src) * a.rstride[k];
-        if (a.kind[k] == IGX_KIND_BYTES) {
+        if (a.dict[k]) {
+            words[w * a.stride + i] = dict_rank(a.dref[a.dict[k] - 1], p, a.width[k]) ^ inv;
+        } else if (a.kind[k] == IGX_KIND_BYTES) {
             for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
             if (a.width[k] == 4) {
@@ -217,12 +453,14 @@ __device__ void sel_state_init(const uint32_t *res, uint32_t nw, uint64_t n, uin
                                const uint64_t *d_n);
 
 // res[2w], res[2w + 1] = AND / OR of word w over k_andor's nb partials (one wave per word),
-// res[2 kw] = the NaN flag, which is cleared for the next sort.  With st (the device top-K)
+// res[2 kw] = the NaN flag, which is cleared for the next sort, res[2 kw + 1] = a void string
+// dictionary, res[2 kw + 2..3] = the device row count (d_n).  With st (the device top-K)
 // the selection state is initialised from them too and its histogram cleared.
 __global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict__ part, uint32_t nb, uint32_t KW,
                                                       uint32_t *__restrict__ res, uint32_t *__restrict__ nan_seen,
                                                       SelState *st, uint64_t n, uint32_t k,
-                                                      const uint64_t *__restrict__ d_n, uint32_t *__restrict__ hist) {
+                                                      const uint64_t *__restrict__ d_n, uint32_t *__restrict__ hist,
+                                                      const uint32_t *__restrict__ dctl = nullptr, uint32_t ndict = 0) {
     __shared__ uint32_t r[2 * MAXW];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t w = wave; w < KW; w += 1024 / 64) {
@@ -244,6 +482,13 @@ __global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict
     if (threadIdx.x == 0) {
         res[2 * KW] = *nan_seen;
         *nan_seen = 0;
+        // the read-back's other words: a void dictionary, the device row count
+        uint32_t dv = 0;
+        for (uint32_t j = 0; j < ndict; ++j) dv |= dctl[4 * j + 1];
+        res[2 * KW + 1] = dv;
+        const uint64_t dn = d_n ? *d_n : 0;
+        res[2 * KW + 2] = (uint32_t)dn;
+        res[2 * KW + 3] = (uint32_t)(dn >> 32);
     }
     if (!st) return;
     for (uint32_t b = threadIdx.x; b < (1u << 12); b += 1024) hist[b] = 0;
@@ -1440,7 +1685,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
                           igx_align(((size_t)256 * nblocks + SCAN_CHUNK - 1) / SCAN_CHUNK * 4, 256);
     constexpr uint32_t ANDOR_BLOCKS = 256;
-    const size_t res_b = igx_align((size_t)KW * 8 + 4, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
+    const size_t res_b = igx_align((size_t)KW * 8 + 16, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
     // Full sorts without float keys may plan their passes on the device (k_lsd_*: no host read at
     // all) with IGX_SORT_DEVPLAN=1.  Measured on C1 (1M rows, 16 live digits) they are slower
@@ -1452,6 +1697,22 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     if (d_nrows && (any_float || (use_sel && !(rowmap && !valid))))
         return igx_fail(ctx, IGX_EINVAL, "sort: a device row count needs integer or string keys (and, for a top-K, "
                                          "a slot list and no nil mask)");
+    // String dictionaries (k_dict_*): host-planned full sorts of many rows, multi-word string
+    // keys of at most DICT_W words.  IGX_SORT_DICT=0 turns them off.
+    uint32_t ndict = 0, dict_of[NSK] = {};
+    const char *dict_env = std::getenv("IGX_SORT_DICT");
+    if (!use_sel && !use_lsd && nrows >= DICT_MIN_ROWS && !(dict_env && std::strcmp(dict_env, "0") == 0))
+        for (uint32_t k = 0; k < nkeys && ndict < (uint32_t)DICT_MAXK; ++k)
+            if (keys[k].kind == IGX_KIND_BYTES && keys[k].words >= 2 && keys[k].words <= (uint32_t)DICT_W &&
+                !keys[k].direct)
+                dict_of[k] = ++ndict;
+    // dictionaries: ctl (16 B each) | slots (each) | values + ranks (each); one memset clears
+    // the ctl words and the slots
+    constexpr uint32_t DSLOTS = 2 * DICT_MAXD;
+    const size_t dict_ctl_b = igx_align((size_t)DICT_MAXK * 16, 256), dict_slot_b = (size_t)DSLOTS * 8;
+    const size_t dict_val_b = igx_align((size_t)DICT_MAXD * DICT_W * 4, 256) + igx_align((size_t)DICT_MAXD * 4, 256);
+    const size_t dict_clear_b = ndict ? dict_ctl_b + ndict * dict_slot_b : 0;
+    const size_t dict_b = ndict ? dict_clear_b + ndict * dict_val_b : 0;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
     static_assert(sizeof(SelState) <= 64 * 4, "SelState fits the 64 words before the selection histogram");
     if (!ctx->nan_word) {
@@ -1480,7 +1741,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         }
     }
     void *s;
-    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b + lsd_b, &s);
+    int rc = igx_scratch(ctx, 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b + lsd_b + dict_b, &s);
     if (rc) return rc;
     char *c = reinterpret_cast<char *>(s);
     uint32_t *W[2] = {reinterpret_cast<uint32_t *>(c), reinterpret_cast<uint32_t *>(c + words_b)};
@@ -1489,6 +1750,25 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     uint32_t *hist = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b);
     uint32_t *scan_part = hist + igx_align((size_t)256 * nblocks, 64);
     uint32_t *res = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b);
+    char *dict_base = c + 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b + lsd_b;
+    uint32_t *dctl = reinterpret_cast<uint32_t *>(dict_base);
+    for (uint32_t k = 0, j = 0; k < nkeys; ++k) {
+        if (!dict_of[k]) continue;
+        char *q = dict_base + dict_clear_b + j * dict_val_b;
+        DictRef &d = ca.dref[j];
+        d.ctl = dctl + 4 * j;
+        d.slot = reinterpret_cast<uint32_t *>(dict_base + dict_ctl_b + j * dict_slot_b);
+        d.keys = reinterpret_cast<uint32_t *>(q);
+        d.rankof = reinterpret_cast<uint32_t *>(q + igx_align((size_t)DICT_MAXD * DICT_W * 4, 256));
+        ++j;
+        d.nw = keys[k].words;
+        d.cap = std::min<uint32_t>(DICT_MAXD, DICT_LDS_WORDS / d.nw);
+        d.mask = DSLOTS - 1;
+    }
+    const uint32_t KW_raw = KW;
+    uint32_t KW_dict = KW_raw;
+    for (uint32_t k = 0; k < nkeys; ++k)
+        if (dict_of[k]) KW_dict -= keys[k].words - 1;
 
     const uint32_t cblocks = (uint32_t)((nrows + TB - 1) / TB);
     ca.nan_seen = ctx->nan_word;
@@ -1496,92 +1776,134 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     for (uint32_t k = 0; k < nkeys && u64_shape; ++k)
         u64_shape = (keys[k].kind == IGX_KIND_UINT || keys[k].kind == IGX_KIND_INT) && keys[k].width == 8 &&
                     keys[k].words == 2 && !keys[k].direct;
-    if (u64_shape) {
-        switch (nkeys) {
-        case 1: hipLaunchKernelGGL(k_compose_u64<1>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
-        case 2: hipLaunchKernelGGL(k_compose_u64<2>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
-        case 3: hipLaunchKernelGGL(k_compose_u64<3>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
-        default: hipLaunchKernelGGL(k_compose_u64<4>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+    uint32_t *hres = nullptr;
+    uint32_t ablocks = 0;
+    // Compose, reduce, read back.  With dictionaries the first attempt composes the ranks; a
+    // void dictionary (more distinct values than it holds) is seen in the read-back, and the
+    // second attempt composes the raw bytes.
+    for (int attempt = 0;; ++attempt) {
+        const bool with_dict = ndict && attempt == 0;
+        KW = with_dict ? KW_dict : KW_raw;
+        for (uint32_t k = 0; k < nkeys; ++k) {
+            ca.dict[k] = with_dict ? dict_of[k] : 0u;
+            ca.words[k] = with_dict && dict_of[k] ? 1u : keys[k].words;
         }
-    } else {
-        hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
-    }
-    if (KW == 0) {   // no key and no position words: the (possibly reversed) row order itself
-        const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
-        IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[0], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
-        IGX_HIP(ctx, hipGetLastError());
-        return IGX_OK;
-    }
-    if (use_lsd) {
-        LsdCtl *ctl = reinterpret_cast<LsdCtl *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b);
-        IGX_HIP(ctx, hipMemsetAsync(ctl, 0, sizeof(LsdCtl), ctx->stream));
-        hipLaunchKernelGGL(k_lsd_h0, dim3(nblocks), dim3(STB), 0, ctx->stream, W[0], KW, stride, nrows, d_nrows, ctl);
-        LsdArgs la{};
-        la.W[0] = W[0];
-        la.W[1] = W[1];
-        la.P[0] = P[0];
-        la.P[1] = P[1];
-        la.stride = stride;
-        la.nmax = nrows;
-        la.d_n = d_nrows;
-        la.status = ctx->lsd_status;
-        la.ctl = ctl;
-        la.KW = KW;
-        for (uint32_t p = 0; p < KW * 4; ++p) {
-            la.pass = p;
-            la.tag = (ctx->lsd_epoch << 5) | p;
-            // pass p works on word KW-1-p/4 and carries the words up to it
-            if (KW - p / 4 <= 4)
-                hipLaunchKernelGGL(k_lsd_pass<4>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
-            else
-                hipLaunchKernelGGL(k_lsd_pass<8>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
+        if (with_dict) {
+            IGX_HIP(ctx, hipMemsetAsync(dict_base, 0, dict_clear_b, ctx->stream));
+            for (uint32_t k = 0; k < nkeys; ++k) {
+                if (!dict_of[k]) continue;
+                DictBuildArgs da{};
+                da.d = ca.dref[dict_of[k] - 1];
+                da.ptr = keys[k].ptr;
+                da.width = keys[k].width;
+                da.rstride = ca.rstride[k];
+                da.rowmap = rowmap;
+                da.valid = valid;
+                da.d_n = d_nrows;
+                da.n = nrows;
+                hipLaunchKernelGGL(k_dict_build, dim3((unsigned)((nrows + DB_ROWS - 1) / DB_ROWS)), dim3(DB_T), 0,
+                                   ctx->stream, da);
+                const size_t lds = ((size_t)da.d.cap * da.d.nw + DICT_MAXD) * 4;
+                static bool attr = false;
+                if (!attr) {
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_dict_rank),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)((DICT_LDS_WORDS + DICT_MAXD) * 4));
+                    attr = true;
+                }
+                hipLaunchKernelGGL(k_dict_rank, dim3(1), dim3(1024), lds, ctx->stream, da.d);
+            }
         }
-        const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
-        hipLaunchKernelGGL(k_lsd_out, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, P[0], P[1], ctl,
-                           nrows, d_nrows, limit, out_perm);
-        IGX_HIP(ctx, hipGetLastError());
-        return IGX_OK;
-    }
-    const uint32_t ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
-    uint32_t *apart = res + igx_align((size_t)KW * 2 + 1, 64);
-    hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
-    if (use_sel && !any_float && rowmap) {
-        // top-K of a table's groups without host round trips (SelState on the device): no float
-        // key, so no NaN check; the first differing bit is found on the device; the position
-        // (first index) makes every composed key unique.  After the compose and AND/OR passes:
-        // the final AND/OR (which also initialises the selection), the first histogram, the
-        // split (each workgroup picks the bin itself) and the one-workgroup finish, which
-        // ranks the k rows itself when their words fit its LDS.
-        uint32_t *acc = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b);
-        uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
-        SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
-        uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
+        if (u64_shape) {
+            switch (nkeys) {
+            case 1: hipLaunchKernelGGL(k_compose_u64<1>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+            case 2: hipLaunchKernelGGL(k_compose_u64<2>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+            case 3: hipLaunchKernelGGL(k_compose_u64<3>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+            default: hipLaunchKernelGGL(k_compose_u64<4>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
+            }
+        } else {
+            hipLaunchKernelGGL(k_compose, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]);
+        }
+        if (KW == 0) {   // no key and no position words: the (possibly reversed) row order itself
+            const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+            IGX_HIP(ctx, hipMemcpyAsync(out_perm, P[0], m * 4, hipMemcpyDeviceToDevice, ctx->stream));
+            IGX_HIP(ctx, hipGetLastError());
+            return IGX_OK;
+        }
+        if (use_lsd) {
+            LsdCtl *ctl = reinterpret_cast<LsdCtl *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b + sel_b);
+            IGX_HIP(ctx, hipMemsetAsync(ctl, 0, sizeof(LsdCtl), ctx->stream));
+            hipLaunchKernelGGL(k_lsd_h0, dim3(nblocks), dim3(STB), 0, ctx->stream, W[0], KW, stride, nrows, d_nrows, ctl);
+            LsdArgs la{};
+            la.W[0] = W[0];
+            la.W[1] = W[1];
+            la.P[0] = P[0];
+            la.P[1] = P[1];
+            la.stride = stride;
+            la.nmax = nrows;
+            la.d_n = d_nrows;
+            la.status = ctx->lsd_status;
+            la.ctl = ctl;
+            la.KW = KW;
+            for (uint32_t p = 0; p < KW * 4; ++p) {
+                la.pass = p;
+                la.tag = (ctx->lsd_epoch << 5) | p;
+                // pass p works on word KW-1-p/4 and carries the words up to it
+                if (KW - p / 4 <= 4)
+                    hipLaunchKernelGGL(k_lsd_pass<4>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
+                else
+                    hipLaunchKernelGGL(k_lsd_pass<8>, dim3(nblocks), dim3(STB), 0, ctx->stream, la);
+            }
+            const uint64_t m = limit ? std::min<uint64_t>(limit, nrows) : nrows;
+            hipLaunchKernelGGL(k_lsd_out, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, ctx->stream, P[0], P[1], ctl,
+                               nrows, d_nrows, limit, out_perm);
+            IGX_HIP(ctx, hipGetLastError());
+            return IGX_OK;
+        }
+        ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
+        uint32_t *apart = res + igx_align((size_t)KW * 2 + 4, 64);
+        hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
+        if (use_sel && !any_float && rowmap) {
+            // top-K of a table's groups without host round trips (SelState on the device): no float
+            // key, so no NaN check; the first differing bit is found on the device; the position
+            // (first index) makes every composed key unique.  After the compose and AND/OR passes:
+            // the final AND/OR (which also initialises the selection), the first histogram, the
+            // split (each workgroup picks the bin itself) and the one-workgroup finish, which
+            // ranks the k rows itself when their words fit its LDS.
+            uint32_t *acc = reinterpret_cast<uint32_t *>(c + 2 * words_b + 2 * pay_b + hist_b + res_b);
+            uint32_t *cnd[2] = {acc + igx_align(limit, 64), acc + igx_align(limit, 64) + stride};
+            SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
+            uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
+            hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res,
+                               ctx->nan_word, stp, nrows, limit, d_nrows, dh, nullptr, 0u);
+            // about 16 rows per thread: each workgroup adds its nonzero bins to the global
+            // histogram, and a skewed table's low bins take one same-address atomic per workgroup
+            const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, nrows / (16 * TB)));
+            hipLaunchKernelGGL(k_sel_hist_d, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, stp, dh);
+            hipLaunchKernelGGL(k_sel_split_d, dim3((uint32_t)((nrows + TILE - 1) / TILE)), dim3(TB), 0, ctx->stream,
+                               W[0], stride, KW, stp, dh, acc, cnd[0]);
+            const bool fused = limit <= 1024 && (uint64_t)limit * KW <= SEL_BINS;   // the k rows' words fit its LDS
+            hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0],
+                               cnd[1], limit, P[0], fused ? out_perm : nullptr);
+            if (!fused)
+                hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
+                                   out_perm, stp);
+            IGX_HIP(ctx, hipGetLastError());
+            return IGX_OK;
+        }
         hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res, ctx->nan_word,
-                           stp, nrows, limit, d_nrows, dh);
-        // about 16 rows per thread: each workgroup adds its nonzero bins to the global
-        // histogram, and a skewed table's low bins take one same-address atomic per workgroup
-        const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, nrows / (16 * TB)));
-        hipLaunchKernelGGL(k_sel_hist_d, dim3(hb), dim3(TB), 0, ctx->stream, W[0], stride, KW, stp, dh);
-        hipLaunchKernelGGL(k_sel_split_d, dim3((uint32_t)((nrows + TILE - 1) / TILE)), dim3(TB), 0, ctx->stream, W[0],
-                           stride, KW, stp, dh, acc, cnd[0]);
-        const bool fused = limit <= 1024 && (uint64_t)limit * KW <= SEL_BINS;   // the k rows' words fit its LDS
-        hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0], cnd[1],
-                           limit, P[0], fused ? out_perm : nullptr);
-        if (!fused)
-            hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
-                               out_perm, stp);
-        IGX_HIP(ctx, hipGetLastError());
-        return IGX_OK;
+                           nullptr, nrows, limit, d_nrows, nullptr, with_dict ? dctl : nullptr, with_dict ? ndict : 0u);
+        // one read-back: the AND/OR words, the NaN flag, a void dictionary, the device row count
+        rc = igx_pinned(ctx, KW_raw * 8 + 16, reinterpret_cast<void **>(&hres));
+        if (rc) return rc;
+        IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8 + 16, hipMemcpyDeviceToHost, ctx->stream));
+        IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (with_dict && hres[2 * KW + 1]) {
+            if (hres[2 * KW + 1] & 2u) return igx_fail(ctx, IGX_EIO, "sort: string dictionary build failed");
+            continue;   // over capacity: compose the raw bytes
+        }
+        break;
     }
-    hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res, ctx->nan_word,
-                       nullptr, nrows, limit, nullptr, nullptr);
-    uint32_t *hres;
-    rc = igx_pinned(ctx, KW * 8 + 16, reinterpret_cast<void **>(&hres));
-    if (rc) return rc;
-    IGX_HIP(ctx, hipMemcpyAsync(hres, res, KW * 8 + 4, hipMemcpyDeviceToHost, ctx->stream));
-    if (d_nrows)   // the device row count rides the same read-back
-        IGX_HIP(ctx, hipMemcpyAsync(hres + 2 * KW + 2, d_nrows, 8, hipMemcpyDeviceToHost, ctx->stream));
-    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     // Go's `<` is unordered on NaN, so getLessFunc (sort.go:125-135) is no strict weak order
     // once a NaN is present and SliceStable's result depends on its insertion-sort blocks and
     // symMerge steps, not on the values alone: no radix order reproduces it, so the passes run
@@ -1650,7 +1972,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
 
     if (d_nrows) {   // the slice's length, read back with the AND/OR words
         uint64_t dn;
-        std::memcpy(&dn, hres + 2 * KW + 2, 8);
+        std::memcpy(&dn, hres + 2 * KW + 2, 8);   // (k_andor_final copies it into res)
         nrows = std::min<uint64_t>(nrows, dn);
         if (nrows == 0) return IGX_OK;
     }

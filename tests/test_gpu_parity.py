@@ -399,6 +399,67 @@ def test_device_planned_sort_matches_host_planned(oracle, E, H, torch, monkeypat
             assert np.array_equal(out, want), (trial, kinds, devplan)
 
 
+def _strings(rng, n, width, distinct):
+    """n strings of `width` (>= 8) bytes drawn from exactly `distinct` values over a 3-letter
+    alphabet (long shared prefixes), of every length from 8 to the field (zero padded, as Go
+    compares them), plus the empty string.  A value's last 8 letters are its index in base 3."""
+    pool = np.zeros((distinct, width), np.uint8)
+    for v in range(1, distinct):
+        ln = int(rng.integers(8, width + 1))
+        pool[v, :ln - 8] = rng.integers(97, 100, ln - 8)
+        pool[v, ln - 8:ln] = [97 + (v // 3 ** d) % 3 for d in range(7, -1, -1)]
+    assert len(np.unique(pool, axis=0)) == distinct
+    return pool[rng.integers(0, distinct, n)]
+
+
+def test_string_dictionary_sort(oracle, E, H, torch, monkeypatch):
+    """String keys of many rows sort through a dictionary of their distinct values (k_dict_*:
+    the rank replaces the bytes, one or two live digits instead of one per byte); a dictionary
+    over capacity (4 096 values of <= 16 bytes, 2 048 of 32) is void and the raw bytes are
+    composed instead.  Same order as IGX_SORT_DICT=0 and as Go's SliceStable restatement: 8-, 12-,
+    16- and 32-byte strings, ascending and descending, with ties broken by position, nil rows, a
+    selection vector with a device count, and exactly-at-capacity / over-capacity value counts."""
+    rng = np.random.default_rng(5)
+    n = 150_000
+    cases = [
+        [(16, 64, False), ("uint32", None, True)],            # C1's shape: comm, -pid
+        [(16, 4096, True)],                                   # exactly the capacity
+        [(16, 4097, False), ("int8", None, False)],           # one over: void, raw bytes
+        [(8, 5000, True), (32, 2000, False)],                 # void (8-byte) + valid (32-byte)
+        [(12, 300, True), (32, 2049, True), ("int64", None, True)],   # the 32-byte one over capacity
+        [(32, 1, False), (16, 3, True)],                      # constant strings
+    ]
+    for ci, spec in enumerate(cases):
+        keys_d, keys_o = [], []
+        for kd, distinct, desc in spec:
+            if isinstance(kd, int):
+                a = _strings(rng, n, kd, distinct)
+                keys_o.append((a, "string", desc))
+            else:
+                a = rng.integers(-40 if kd.startswith("int") else 0, 40, n).astype(kd)
+                keys_o.append((a, kd, desc))
+            keys_d.append((H.to_device(a), desc))
+        valid = (rng.random(n) < 0.93).astype(np.uint8) if ci % 2 else None
+        vd = None if valid is None else H.to_device(valid)
+        ref = oracle.go_sort_entries(keys_o, n, valid=valid)
+        got = H.host(E.sort_perm(keys_d, n, valid=vd))
+        monkeypatch.setenv("IGX_SORT_DICT", "0")
+        raw = H.host(E.sort_perm(keys_d, n, valid=vd))
+        monkeypatch.delenv("IGX_SORT_DICT")
+        assert np.array_equal(raw, ref), ci
+        assert np.array_equal(got, ref), ci
+        # a selection of m rows with its count on the device (FilterEntries' pending view)
+        sel = np.sort(rng.choice(n, n // 2 + 1, replace=False)).astype(np.uint32)[::-1].copy()
+        m = len(sel)
+        cap = torch.full((n,), 0x7FFFFFFF, dtype=torch.int32, device="cuda").view(torch.uint32)
+        cap[:m] = H.to_device(sel)
+        cnt = torch.tensor([m], dtype=torch.int64, device="cuda").view(torch.uint64)
+        sub = [(a[sel], kd, d) for a, kd, d in keys_o]
+        want = sel[oracle.go_sort_entries(sub, m, valid=None if valid is None else valid[sel]).astype(np.int64)]
+        out = H.host(E.sort_perm(keys_d, n, valid=vd, rowmap=cap, d_count=cnt))[:m]
+        assert np.array_equal(out, want), ci
+
+
 @pytest.mark.parametrize("devplan", [False, True])
 def test_filter_then_sort_pending_count(oracle, E, H, igx, torch, monkeypatch, devplan):
     """C1's step as the bench runs it: FilterEntries leaves its survivor count on the device and
