@@ -208,9 +208,14 @@ int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, const char *con
  * Float keys compare as Go's `<` does: -0 == +0, -Inf < finite < +Inf; a NaN in a float key
  * of a non-nil row makes the comparison unordered (no strict weak order, so SliceStable's
  * output depends on its merge steps) and the call returns IGX_ENOTSUP.
- * out_perm (device u32, nrows).  Asynchronous when no key is a float and the composed key is at
- * most 8 words (the passes are planned on the device); otherwise synchronises once (key range
- * and NaN scan). */
+ * out_perm (device u32, nrows).  Synchronises once: the digit plan's read-back (which bytes of
+ * the composed key vary, the NaN flag, a device row count); IGX_SORT_DEVPLAN=1 plans full sorts
+ * of at most 8 composed words without float keys on the device instead (no read-back; slower
+ * at 1M rows).  String keys of 5..32 bytes in full sorts of >= 65 536 rows sort
+ * by their rank in a dictionary of their distinct values (at most 4 096; 2 048 for 32 bytes),
+ * built on the device -- the same order, a few radix passes instead of one per live byte;
+ * more distinct values: the raw bytes, after one more read-back.  IGX_SORT_DICT=0 turns the
+ * dictionaries off. */
 int igx_sort_perm(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows,
                   const uint64_t *pos, const uint8_t *valid, uint32_t *out_perm);
 
@@ -225,11 +230,11 @@ int igx_sort_perm_ex(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint
 
 /* igx_sort_perm_ex when the row count lives on the device: the slice is rows [0, *d_nrows) of
  * the selection vector, nrows_max its upper bound (d_nrows: device u64, e.g. igx_filter's
- * out_n) -- FilterEntries' count feeds SortEntries without a host round trip.  Composed keys
- * of at most 8 words and no float key (a NaN would need the host's decision): otherwise
- * IGX_EINVAL.  out_perm (device u32, nrows_max) holds the sorted rowmap values in its first
- * *d_nrows entries.  Asynchronous: no host synchronisation at all (the passes are planned on
- * the device).  igx_sort_perm / _ex plan the same way whenever their keys allow it. */
+ * out_n) -- FilterEntries' count feeds SortEntries without a read-back of its own: it rides
+ * the digit plan's read-back (none with IGX_SORT_DEVPLAN=1).  No float key (a NaN would need
+ * the host's decision before the count is known), and a top-K needs a slot list and no nil
+ * mask: otherwise IGX_EINVAL.  out_perm (device u32, nrows_max) holds the sorted rowmap values
+ * in its first *d_nrows entries. */
 int igx_sort_perm_dn(igx_ctx *ctx, const igx_sortkey *keys, uint32_t nkeys, uint64_t nrows_max,
                      const uint64_t *d_nrows, const uint64_t *pos, const uint8_t *valid, const uint32_t *rowmap,
                      uint32_t *out_perm);

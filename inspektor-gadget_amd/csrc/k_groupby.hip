@@ -59,6 +59,12 @@
 #else
 #define IGX_STREAM_LOAD(p) (*(p))
 #endif
+// a stream load, non-temporal (IGX_STREAM_LOAD) unless the caller asks for a plain one
+template <bool NT, class T>
+__device__ __forceinline__ T stream_ld(const T *p) {
+    if constexpr (NT) return IGX_STREAM_LOAD(p);
+    else return *p;
+}
 
 namespace {
 
@@ -218,7 +224,7 @@ struct StaticLayout {
     static constexpr int KW = off(NC);
     static constexpr bool is_static = true;
 
-    template <int c>
+    template <int c, bool NT>
     __device__ __forceinline__ static void load_col(const GbArgs &a, uint64_t row, uint32_t *k) {
         constexpr int w = Ws[c];
         constexpr int o = off(c);
@@ -227,31 +233,32 @@ struct StaticLayout {
         // table's key records out of the caches
         if constexpr (w == 16) {
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u q = IGX_STREAM_LOAD(reinterpret_cast<const v4u *>(p) + row);
+            const v4u q = stream_ld<NT>(reinterpret_cast<const v4u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y; k[o + 2] = q.z; k[o + 3] = q.w;
         } else if constexpr (w == 8) {
             typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-            const v2u q = IGX_STREAM_LOAD(reinterpret_cast<const v2u *>(p) + row);
+            const v2u q = stream_ld<NT>(reinterpret_cast<const v2u *>(p) + row);
             k[o] = q.x; k[o + 1] = q.y;
         } else if constexpr (w == 4) {
-            k[o] = IGX_STREAM_LOAD(reinterpret_cast<const uint32_t *>(p) + row);
+            k[o] = stream_ld<NT>(reinterpret_cast<const uint32_t *>(p) + row);
         } else if constexpr (w == 2) {
-            k[o] = IGX_STREAM_LOAD(reinterpret_cast<const uint16_t *>(p) + row);
+            k[o] = stream_ld<NT>(reinterpret_cast<const uint16_t *>(p) + row);
         } else if constexpr (w == 1) {
-            k[o] = IGX_STREAM_LOAD(p + row);
+            k[o] = stream_ld<NT>(p + row);
         } else {
             static_assert(w % 4 == 0, "key widths other than 1/2 must be multiples of 4");
 #pragma unroll
             for (int j = 0; j < w / 4; ++j) k[o + j] = reinterpret_cast<const uint32_t *>(p + row * w)[j];
         }
     }
-    template <size_t... I>
+    template <bool NT, size_t... I>
     __device__ __forceinline__ static void load_all(const GbArgs &a, uint64_t row, uint32_t *k,
                                                     std::index_sequence<I...>) {
-        (load_col<(int)I>(a, row, k), ...);
+        (load_col<(int)I, NT>(a, row, k), ...);
     }
+    template <bool NT = true>
     __device__ __forceinline__ static void load(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
-        load_all(a, row, k, std::make_index_sequence<NC>{});
+        load_all<NT>(a, row, k, std::make_index_sequence<NC>{});
     }
 };
 
@@ -259,6 +266,7 @@ template <int KWG>
 struct GenericLayout {
     static constexpr int KW = KWG;
     static constexpr bool is_static = false;
+    template <bool NT = true>
     __device__ __forceinline__ static void load(const GbArgs &a, uint64_t row, uint32_t (&k)[KW]) {
 #pragma unroll
         for (int w = 0; w < KW; ++w) {
@@ -508,8 +516,9 @@ __device__ __forceinline__ bool lds_key_eq(const LdsCache<KW> &c, uint32_t e, co
 // combined.  A load whose value is used inside a branch forces the wait into that branch,
 // so each guarded column used to cost a memory round trip of its own; issued together
 // they retire under one wait.
+template <bool NT = true>
 __device__ __forceinline__ uint32_t ldd(const uint8_t *base, uint64_t off) {
-    return IGX_STREAM_LOAD(reinterpret_cast<const uint32_t *>(base + (off & ~3ull)));
+    return stream_ld<NT>(reinterpret_cast<const uint32_t *>(base + (off & ~3ull)));
 }
 
 // zero-extended value of `width` bytes from the aligned dwords lo (holding its first byte)
@@ -529,27 +538,33 @@ struct RowRaw {
     uint32_t vraw, plo[PMAX], phi[PMAX], vlo[NA], vhi[NA], clo[NA], chi[NA];
 };
 
-template <class L, int NA>
+template <class L, int NA, bool NT = true>
 __device__ __forceinline__ void issue_row(const GbArgs &a, uint64_t row, RowRaw<L, NA> &R) {
     // unconditional loads; slots with nothing to load read dword 0 of the dummy column
     // (width 0: one cached line for the whole wave)
-    R.vraw = ldd(a.validp, row * a.validw);
+    R.vraw = ldd<NT>(a.validp, row * a.validw);
 #pragma unroll
     for (int p = 0; p < PMAX; ++p) {
         const uint64_t b = row * a.pldw[p];
-        R.plo[p] = ldd(a.pptr[p], b);
-        R.phi[p] = ldd(a.pptr[p], b + a.phioff[p]);
+        R.plo[p] = ldd<NT>(a.pptr[p], b);
+        R.phi[p] = ldd<NT>(a.pptr[p], b + a.phioff[p]);
     }
-    L::load(a, row, R.k);
+    L::template load<NT>(a, row, R.k);
 #pragma unroll
     for (int x = 0; x < NA; ++x) {
         const uint64_t bv = row * a.vldw[x], bc = row * a.cldw[x];
-        R.vlo[x] = ldd(a.vptr[x], bv);
-        R.vhi[x] = ldd(a.vptr[x], bv + a.vhioff[x]);
-        R.clo[x] = ldd(a.cptr[x], bc);
-        R.chi[x] = ldd(a.cptr[x], bc + a.chioff[x]);
+        R.vlo[x] = ldd<NT>(a.vptr[x], bv);
+        R.vhi[x] = ldd<NT>(a.vptr[x], bv + a.vhioff[x]);
+        R.clo[x] = ldd<NT>(a.cptr[x], bc);
+        R.chi[x] = ldd<NT>(a.cptr[x], bc + a.chioff[x]);
     }
 }
+
+// The cached kernel's stream loads: non-temporal, so the event stream does not push the
+// table's key records out of the caches -- except for the top-file key, whose kernel is faster
+// with plain loads (C5 5.94-5.98 -> 5.84 ms with a plain-load build, C2 3.7 -> 4.0).
+template <class L>
+constexpr bool cached_stream_nt() { return !std::is_same<L, StaticLayout<8, 4, 4, 4>>::value; }
 
 // aggregates reading a column an earlier one already loaded reuse its value
 template <int NA>
@@ -1394,13 +1409,13 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
         uint64_t base = (uint64_t)blockIdx.x * PTB + wave * 64;
         RowRaw<L, NA> R;
         uint32_t nmiss = 0;
-        if (base < a.n) issue_row<L, NA>(a, min(base + lane, a.n - 1), R);
+        if (base < a.n) issue_row<L, NA, cached_stream_nt<L>()>(a, min(base + lane, a.n - 1), R);
         for (; base < a.n; base += stride) {
             const uint64_t row = base + lane;
             uint32_t k[KW];
             uint64_t v[NA];
             bool ok = decode_row<L, NA>(a, row, R, k, v) && row < a.n;
-            if (base + stride < a.n) issue_row<L, NA>(a, min(base + stride + lane, a.n - 1), R);
+            if (base + stride < a.n) issue_row<L, NA, cached_stream_nt<L>()>(a, min(base + stride + lane, a.n - 1), R);
             const uint64_t h = hash_key<KW>(k);
             if (DBG && (a.dbg & 1u)) {   // diagnostics: load + hash only
                 if (ok && h == 0x1234567ull && v[0] == 7) atomicAdd(a.dbg_cnt + 3, 1ull);   // keep live

@@ -60,21 +60,25 @@ __device__ __forceinline__ uint32_t be_word(const uint8_t *p, uint32_t width, ui
 // 16 passes).  When the key has few distinct values, the sort replaces it by its rank among
 // them: equal strings get equal ranks and the ranks keep the strings' byte order, so the
 // stable LSD passes over the rank produce exactly the order of the passes over the bytes --
-// with one or two live digits instead of a dozen.  k_dict_build collects the distinct values
-// (an open-addressed table of {tag, index} slots; the values themselves in claim order),
-// k_dict_rank sorts them in one workgroup's LDS (bitonic, over indices) and k_compose looks
-// every row's rank up.  More distinct values than the dictionary holds void it (ctl[1]); the
-// host then composes the raw bytes (one more read-back, launch_sort_perm).
+// with one or two live digits instead of a dozen.  k_dict_build collects the distinct values:
+// each workgroup first in an LDS table over its own rows, then only those into the global
+// table (an open-addressed table of {tag, index} slots, the values in claim order -- a few
+// values over a million rows would otherwise send every row's L1-bypassing probe to the same
+// few L2 lines: 0.91 ms for C1 measured); k_dict_rank sorts the distinct values in one
+// workgroup's LDS (bitonic, over indices) and writes each one's rank next to it; k_compose
+// looks every row's rank up.  More distinct values than the dictionary holds void it (ctl[1]);
+// the host then composes the raw bytes (one more read-back, launch_sort_perm).
 constexpr int DICT_W = 8;                // key words a dictionary takes (strings of <= 32 bytes)
 constexpr uint32_t DICT_MAXD = 4096;     // distinct values (power of two)
 constexpr uint32_t DICT_LDS_WORDS = 16384;   // k_dict_rank: distinct values x words in LDS
 constexpr int DICT_MAXK = 4;             // dictionary keys per sort
 constexpr uint64_t DICT_MIN_ROWS = 1u << 16;
+constexpr uint32_t DENT = 16;            // words per dictionary entry (value, rank, padding)
 
 struct DictRef {
     uint32_t *slot;     // 2 x (mask + 1): {tag (0 empty, 1 being written, else hash | 2), index}
-    uint32_t *keys;     // cap x nw: the distinct values' words, in claim order
-    uint32_t *rankof;   // cap: rank of value i among the distinct values
+    uint32_t *keys;     // cap x DENT: the distinct values in claim order, one 64-B line each:
+                        // the value's words, then (k_dict_rank) its rank at word DICT_W
     uint32_t *ctl;      // [0] distinct values claimed, [1] void (over capacity)
     uint32_t mask, cap, nw;
 };
@@ -125,7 +129,7 @@ __device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint3
                 }
 #pragma unroll
                 for (int j = 0; j < DICT_W; ++j)
-                    if ((uint32_t)j < d.nw) d.keys[(uint64_t)idx * d.nw + j] = k[j];
+                    if ((uint32_t)j < d.nw) d.keys[(uint64_t)idx * DENT + j] = k[j];
                 d.slot[2 * s + 1] = idx;
                 __hip_atomic_store(&d.slot[2 * s], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 return;
@@ -140,7 +144,7 @@ __device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint3
         }
         if (t == tg) {
             const uint32_t idx = d.slot[2 * s + 1];
-            if (dict_eq(d.keys + (uint64_t)idx * d.nw, k, d.nw)) return;
+            if (dict_eq(d.keys + (uint64_t)idx * DENT, k, d.nw)) return;
         }
         s = (s + 1) & d.mask;
         ++probes;
@@ -148,12 +152,10 @@ __device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint3
     atomicOr(&d.ctl[1], 2u);   // no free slot (cannot happen: at most half the slots are claimed)
 }
 
-// Each workgroup first collects the distinct values of its DB_ROWS rows in LDS and then
-// inserts only those into the global table: a few distinct values over a million rows would
-// otherwise send every row's (L1-bypassing) probe to the same few L2 lines (measured: 0.91 ms
-// for C1's 0.87M rows and 64 names).  A block with more than DL_CAP distinct values sends the
-// rest straight to the global table.
-constexpr uint32_t DB_T = 1024, DB_RPT = 4, DB_ROWS = DB_T * DB_RPT;
+// The collection: DB_RPT rows per thread per step (their loads in flight together); a
+// workgroup with more than DL_CAP distinct values (or a full LDS table) sends the rest
+// straight to the global table.
+constexpr uint32_t DB_T = 1024, DB_RPT = 8, DB_ROWS = DB_T * DB_RPT;
 constexpr uint32_t DL_SLOTS = 2048, DL_CAP = 1024, DL_NONE = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
@@ -186,7 +188,9 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
         if (!live[r]) continue;
         const uint32_t h = dict_hash(k[r], d.nw), tg = h | 2u;
         uint32_t s = h & (DL_SLOTS - 1);
-        bool global = false;
+        // global unless the value is (now) in this workgroup's list: a full list (DL_NONE) or a
+        // full table sends it to the global table directly
+        bool global = true;
         for (uint32_t probes = 0, spins = 0; probes < DL_SLOTS;) {
             const uint32_t t = __hip_atomic_load(&ltag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (t == 0u) {
@@ -198,9 +202,9 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
                             if ((uint32_t)j < d.nw) lval[li * d.nw + j] = k[r][j];
                         lhash[li] = h;
                         lidx[s] = li;
+                        global = false;
                     } else {
                         lidx[s] = DL_NONE;   // this value (and any sharing its hash) goes global
-                        global = true;
                     }
                     __hip_atomic_store(&ltag[s], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
@@ -213,8 +217,11 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
             }
             if (t == tg) {
                 const uint32_t li = lidx[s];
-                if (li == DL_NONE) { global = true; break; }
-                if (dict_eq(lval + li * d.nw, k[r], d.nw)) break;
+                if (li == DL_NONE) break;
+                if (dict_eq(lval + li * d.nw, k[r], d.nw)) {
+                    global = false;
+                    break;
+                }
             }
             s = (s + 1) & (DL_SLOTS - 1);
             ++probes;
@@ -231,8 +238,10 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
     }
 }
 
-// One workgroup: the distinct values into LDS, a bitonic sort of their indices (the values are
-// distinct, so no tie order to keep), rankof[index] = position.
+// k_dict_rank (one workgroup): the distinct values into LDS, a bitonic sort of their indices
+// (the values are distinct, so no tie order to keep), the rank of value i next to its words.
+// (Run by k_dict_build's last workgroup instead: 39 vs 23 + 13 us on C1 -- the collection's
+// workgroups then hold the ranking's 80 KB of LDS.)
 __global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
     extern __shared__ uint32_t dl[];
     if (d.ctl[1]) return;   // void: the host composes the raw bytes
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
     uint32_t N = 2;
     while (N < D) N <<= 1;
     uint32_t *kv = dl, *ix = dl + (size_t)d.cap * nw;
-    for (uint32_t t = threadIdx.x; t < D * nw; t += 1024) kv[t] = d.keys[t];
+    for (uint32_t t = threadIdx.x; t < D * nw; t += 1024) kv[t] = d.keys[(t / nw) * DENT + t % nw];
     for (uint32_t t = threadIdx.x; t < N; t += 1024) ix[t] = t;
     __syncthreads();
     // greater(a, b): pad indices (>= D) sort last
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
             __syncthreads();
         }
     }
-    for (uint32_t t = threadIdx.x; t < D; t += 1024) d.rankof[ix[t]] = t;
+    for (uint32_t t = threadIdx.x; t < D; t += 1024) d.keys[(uint64_t)ix[t] * DENT + DICT_W] = t;
 }
 
 // the rank of a row's value (k_compose; the value is in the dictionary unless it is void)
@@ -281,7 +290,12 @@ __device__ __forceinline__ uint32_t dict_rank(const DictRef &d, const uint8_t *p
         if (t == 0u) break;
         if (t == tg) {
             const uint32_t idx = d.slot[2 * s + 1];
-            if (idx < d.cap && dict_eq(d.keys + (uint64_t)idx * d.nw, k, d.nw)) return d.rankof[idx];
+            if (idx < d.cap) {   // the entry's line: value words and rank
+                const uint4 *e = reinterpret_cast<const uint4 *>(d.keys + (uint64_t)idx * DENT);
+                const uint4 q0 = e[0], q1 = e[1], q2 = e[2];
+                const uint32_t v[DICT_W] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+                if (dict_eq(v, k, d.nw)) return q2.x;
+            }
         }
     }
     return 0u;   // only when the dictionary is void (the host then discards this compose)
@@ -627,23 +641,24 @@ constexpr uint32_t SCAN_FREE_TILES = 512;
 
 // this tile's base of every digit from the raw counts, stored tile-major ([tile][digit]: a
 // wave reads 64 digits of one tile in one request): the block's four 256-thread quarters each
-// sum digit t's counts over a quarter of the tiles (before this one, and all), 16 loads in
+// sum digit t's counts over a quarter of the tiles (before this one, and all), TDB_U loads in
 // flight per thread; the quarters' sums meet in LDS and the digit totals are scanned across
 // the first 256 threads -- the three scan kernels a pass would otherwise need.  Called by the
 // whole block; threads 0..255 get digit t's base, the others 0.  tmp: 4 + 2 x 1024 words.
 constexpr uint32_t NPART = STB / 256;   // 256-thread parts of a radix block
+constexpr int TDB_U = 16;               // count loads in flight per thread (32: no faster on C1)
 __device__ __forceinline__ uint32_t tile_digit_base(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t *tmp) {
     const uint32_t t = threadIdx.x & 255u, part = threadIdx.x >> 8, lane = t & 63, wave = t >> 6;
     const uint32_t me = blockIdx.x;
     const uint32_t q0 = (uint32_t)((uint64_t)nb * part / NPART), q1 = (uint32_t)((uint64_t)nb * (part + 1) / NPART);
     uint32_t pre = 0, tot = 0;
     uint32_t q = q0;
-    for (; q + 16 <= q1; q += 16) {
-        uint32_t v[16];
+    for (; q + TDB_U <= q1; q += TDB_U) {
+        uint32_t v[TDB_U];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = cnt[(uint64_t)(q + u) * 256 + t];
+        for (int u = 0; u < TDB_U; ++u) v[u] = cnt[(uint64_t)(q + u) * 256 + t];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < TDB_U; ++u) {
             tot += v[u];
             if (q + u < me) pre += v[u];
         }
@@ -1710,7 +1725,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     // the ctl words and the slots
     constexpr uint32_t DSLOTS = 2 * DICT_MAXD;
     const size_t dict_ctl_b = igx_align((size_t)DICT_MAXK * 16, 256), dict_slot_b = (size_t)DSLOTS * 8;
-    const size_t dict_val_b = igx_align((size_t)DICT_MAXD * DICT_W * 4, 256) + igx_align((size_t)DICT_MAXD * 4, 256);
+    const size_t dict_val_b = (size_t)DICT_MAXD * DENT * 4;
     const size_t dict_clear_b = ndict ? dict_ctl_b + ndict * dict_slot_b : 0;
     const size_t dict_b = ndict ? dict_clear_b + ndict * dict_val_b : 0;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
@@ -1759,7 +1774,6 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         d.ctl = dctl + 4 * j;
         d.slot = reinterpret_cast<uint32_t *>(dict_base + dict_ctl_b + j * dict_slot_b);
         d.keys = reinterpret_cast<uint32_t *>(q);
-        d.rankof = reinterpret_cast<uint32_t *>(q + igx_align((size_t)DICT_MAXD * DICT_W * 4, 256));
         ++j;
         d.nw = keys[k].words;
         d.cap = std::min<uint32_t>(DICT_MAXD, DICT_LDS_WORDS / d.nw);
