@@ -86,7 +86,9 @@ def parse(argv=None):
                    help="other configs to run after the headline ('' = none)")
     p.add_argument("--config-events", type=int, default=125_000_000,
                    help="events per GPU for C3/C4/C5 (the 8-GPU configs' 1B / 8)")
-    p.add_argument("--config-steps", type=int, default=5)
+    p.add_argument("--config-steps", type=int, default=20,
+                   help="timed steps per other config (C1 at 5 steps: 0.20-0.22 ms, at 50: 0.17 -- the "
+                        "closing synchronisation weighs on a 0.2 ms step)")
     p.add_argument("--no-check", dest="check", action="store_false",
                    help="skip the post-run check of each config's last timed interval against the oracle")
     p.add_argument("--transport", choices=("igx", "torch"), default="torch",
