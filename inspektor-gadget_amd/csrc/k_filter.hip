@@ -4,10 +4,11 @@
 // every predicate is `(field OP ref) != negate`, predicates AND together, nil rows are
 // skipped, and survivors keep input order.
 //
-// Three launches, each a straight HBM stream:
+// Two or three launches, each a straight HBM stream:
 //   mark     one pass over the predicate columns; one 64-bit ballot word per wave-row-group
 //            (1 bit per row) + one survivor count per 1024-row tile
-//   scan     exclusive scan of the tile counts (one workgroup)
+//   scan     exclusive scan of the tile counts (one workgroup; up to 16M rows the compaction
+//            sums its tile's predecessors itself instead)
 //   compact  re-reads only the bitmask (n/8 bytes) and writes the u32 row ids
 // Algorithmic bytes per row = sum of predicate column widths + 4 per survivor.
 #include "k_common.h"
@@ -190,6 +191,43 @@ __global__ __launch_bounds__(TB) void k_filter_compact(const uint64_t *__restric
     }
 }
 
+// k_scan_counts + k_filter_compact in one launch, for up to SF_MAX_TILES tiles: each tile
+// sums the counts of the tiles before it itself (at most SF_MAX_TILES / TB loads per thread),
+// and the last tile writes the survivor count.
+constexpr uint64_t SF_MAX_TILES = 16384;
+__global__ __launch_bounds__(TB) void k_filter_compact_sf(const uint64_t *__restrict__ mask,
+                                                          const uint32_t *__restrict__ cnt, uint64_t ntiles,
+                                                          uint32_t *__restrict__ out, uint64_t *__restrict__ out_n) {
+    __shared__ uint32_t wpre[WPT];
+    __shared__ uint64_t red[TB / 64];
+    const uint64_t tile = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t s = 0;
+#pragma unroll 4
+    for (uint64_t i = threadIdx.x; i < tile; i += TB) s += cnt[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[wave] = s;
+    if (threadIdx.x < WPT) {
+        uint32_t p = 0;
+#pragma unroll
+        for (int w = 0; w < WPT; ++w)
+            if (w < (int)threadIdx.x) p += __popcll(mask[tile * WPT + w]);
+        wpre[threadIdx.x] = p;
+    }
+    __syncthreads();
+    uint64_t base = 0;
+#pragma unroll
+    for (int w = 0; w < TB / 64; ++w) base += red[w];
+    if (tile == ntiles - 1 && threadIdx.x == 0) *out_n = base + cnt[tile];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+        const uint32_t k = j * TB + threadIdx.x;   // row within tile
+        const uint32_t w = k >> 6;                 // == j*4 + wave
+        const uint64_t m = mask[tile * WPT + w];
+        if ((m >> lane) & 1ull) out[base + wpre[w] + __popcll(m & lanemask_lt())] = (uint32_t)(tile * TILE + k);
+    }
+}
+
 }  // namespace
 
 int launch_filter(igx_ctx *ctx, const DevPreds &dp, const uint8_t *valid, uint64_t nrows,
@@ -235,9 +273,14 @@ int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, ui
             hipLaunchKernelGGL(k_filter_mark, dim3(ntiles), dim3(TB), 0, ctx->stream, dps[c], valid, nrows,
                                mask, cnt, any, c > 0 ? 1u : 0u, nil_bit);
     }
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, ctx->stream, cnt, ntiles, off, out_n);
-    hipLaunchKernelGGL(k_filter_compact, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, off, nrows,
-                       out_idx);
+    if (ntiles <= SF_MAX_TILES) {
+        hipLaunchKernelGGL(k_filter_compact_sf, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, cnt, ntiles, out_idx,
+                           out_n);
+    } else {
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, ctx->stream, cnt, ntiles, off, out_n);
+        hipLaunchKernelGGL(k_filter_compact, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, off, nrows,
+                           out_idx);
+    }
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }
