@@ -80,6 +80,7 @@ struct DictRef {
     uint32_t *keys;     // cap x DENT: the distinct values in claim order, one 64-B line each:
                         // the value's words, then (k_dict_rank) its rank at word DICT_W
     uint32_t *ctl;      // [0] distinct values claimed, [1] void (over capacity)
+    uint32_t *rowidx;   // per slice row (k_dict_build): its value's index (k_compose reads the rank there)
     uint32_t mask, cap, nw;
 };
 
@@ -112,10 +113,12 @@ __device__ __forceinline__ bool dict_eq(const uint32_t *v, const uint32_t (&k)[D
     return diff == 0;
 }
 
-// Insert a value into the global table (the value's hash h).  One probe per iteration: a lane
-// that finds its slot being written looks again next iteration, so a claimer of the same wave
-// (which publishes within its own iteration) is never waited for inside a branch.
-__device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint32_t h) {
+// Insert a value into the global table (the value's hash h); returns its index (DL_NONE: the
+// dictionary is void).  One probe per iteration: a lane that finds its slot being written
+// looks again next iteration, so a claimer of the same wave (which publishes within its own
+// iteration) is never waited for inside a branch.
+constexpr uint32_t DL_NONE = 0xFFFFFFFFu;
+__device__ uint32_t dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint32_t h) {
     const uint32_t tg = h | 2u;
     uint32_t s = h & d.mask;
     for (uint32_t probes = 0, spins = 0; probes <= d.mask;) {
@@ -125,44 +128,46 @@ __device__ void dict_insert(const DictRef &d, const uint32_t (&k)[DICT_W], uint3
                 const uint32_t idx = atomicAdd(&d.ctl[0], 1u);
                 if (idx >= d.cap) {   // over capacity: the dictionary is void (the slot stays busy)
                     atomicOr(&d.ctl[1], 1u);
-                    return;
+                    return DL_NONE;
                 }
 #pragma unroll
                 for (int j = 0; j < DICT_W; ++j)
                     if ((uint32_t)j < d.nw) d.keys[(uint64_t)idx * DENT + j] = k[j];
                 d.slot[2 * s + 1] = idx;
                 __hip_atomic_store(&d.slot[2 * s], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                return;
+                return idx;
             }
             continue;   // lost the claim: read the slot again
         }
         if (t == 1u) {   // being written
-            if (__hip_atomic_load(&d.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-            if (++spins > (1u << 20)) { atomicOr(&d.ctl[1], 2u); return; }
+            if (__hip_atomic_load(&d.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return DL_NONE;
+            if (++spins > (1u << 20)) { atomicOr(&d.ctl[1], 2u); return DL_NONE; }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
         if (t == tg) {
             const uint32_t idx = d.slot[2 * s + 1];
-            if (dict_eq(d.keys + (uint64_t)idx * DENT, k, d.nw)) return;
+            if (dict_eq(d.keys + (uint64_t)idx * DENT, k, d.nw)) return idx;
         }
         s = (s + 1) & d.mask;
         ++probes;
     }
     atomicOr(&d.ctl[1], 2u);   // no free slot (cannot happen: at most half the slots are claimed)
+    return DL_NONE;
 }
 
-// The collection: DB_RPT rows per thread per step (their loads in flight together); a
-// workgroup with more than DL_CAP distinct values (or a full LDS table) sends the rest
-// straight to the global table.
+// The collection: DB_RPT rows per thread (their loads in flight together; one workgroup per
+// DB_ROWS rows); a workgroup with more than DL_CAP distinct values (or a full LDS table)
+// sends the rest straight to the global table.  Every row's value index goes to rowidx.
 constexpr uint32_t DB_T = 1024, DB_RPT = 8, DB_ROWS = DB_T * DB_RPT;
-constexpr uint32_t DL_SLOTS = 2048, DL_CAP = 1024, DL_NONE = 0xFFFFFFFFu;
+constexpr uint32_t DL_SLOTS = 2048, DL_CAP = 1024, DL_GLOBAL = 0x80000000u;
 
 __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
     __shared__ uint32_t ltag[DL_SLOTS];   // 0 empty, 1 being written, else hash | 2
     __shared__ uint32_t lidx[DL_SLOTS];   // the value's local index, DL_NONE: it went global
     __shared__ uint32_t lval[DL_CAP * DICT_W];
     __shared__ uint32_t lhash[DL_CAP];
+    __shared__ uint32_t lglob[DL_CAP];    // local value -> its global index
     __shared__ uint32_t lcount;
     const DictRef &d = a.d;
     for (uint32_t t = threadIdx.x; t < DL_SLOTS; t += DB_T) ltag[t] = 0;
@@ -183,8 +188,10 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
 #pragma unroll
         for (int j = 0; j < DICT_W; ++j) k[r][j] = live[r] && (uint32_t)j < d.nw ? be_word(p, a.width, j) : 0u;
     }
+    uint32_t lr[DB_RPT];   // the row's local index, or DL_GLOBAL | its global index
 #pragma unroll
     for (int r = 0; r < (int)DB_RPT; ++r) {
+        lr[r] = DL_NONE;
         if (!live[r]) continue;
         const uint32_t h = dict_hash(k[r], d.nw), tg = h | 2u;
         uint32_t s = h & (DL_SLOTS - 1);
@@ -202,6 +209,7 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
                             if ((uint32_t)j < d.nw) lval[li * d.nw + j] = k[r][j];
                         lhash[li] = h;
                         lidx[s] = li;
+                        lr[r] = li;
                         global = false;
                     } else {
                         lidx[s] = DL_NONE;   // this value (and any sharing its hash) goes global
@@ -219,6 +227,7 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
                 const uint32_t li = lidx[s];
                 if (li == DL_NONE) break;
                 if (dict_eq(lval + li * d.nw, k[r], d.nw)) {
+                    lr[r] = li;
                     global = false;
                     break;
                 }
@@ -226,7 +235,7 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
             s = (s + 1) & (DL_SLOTS - 1);
             ++probes;
         }
-        if (global) dict_insert(d, k[r], h);
+        if (global) lr[r] = DL_GLOBAL | dict_insert(d, k[r], h);
     }
     __syncthreads();
     const uint32_t nloc = min(lcount, DL_CAP);
@@ -234,7 +243,14 @@ __global__ __launch_bounds__(DB_T) void k_dict_build(DictBuildArgs a) {
         uint32_t v[DICT_W];
 #pragma unroll
         for (int j = 0; j < DICT_W; ++j) v[j] = (uint32_t)j < d.nw ? lval[li * d.nw + j] : 0u;
-        dict_insert(d, v, lhash[li]);
+        lglob[li] = dict_insert(d, v, lhash[li]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < (int)DB_RPT; ++r) {
+        if (!live[r]) continue;
+        const uint32_t x = lr[r];
+        d.rowidx[base + (uint64_t)r * DB_T] = (x & DL_GLOBAL) ? (x == DL_NONE ? DL_NONE : x & ~DL_GLOBAL) : lglob[x];
     }
 }
 
@@ -246,12 +262,47 @@ __global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
     extern __shared__ uint32_t dl[];
     if (d.ctl[1]) return;   // void: the host composes the raw bytes
     const uint32_t D = min(d.ctl[0], d.cap), nw = d.nw;
+    if (D == 0) return;   // no live row (an empty slice, every row nil): nothing to rank
     uint32_t N = 2;
     while (N < D) N <<= 1;
     uint32_t *kv = dl, *ix = dl + (size_t)d.cap * nw;
     for (uint32_t t = threadIdx.x; t < D * nw; t += 1024) kv[t] = d.keys[(t / nw) * DENT + t % nw];
     for (uint32_t t = threadIdx.x; t < N; t += 1024) ix[t] = t;
     __syncthreads();
+    if (D <= 256) {
+        // few values: P threads per value each count the values below it among every P-th one
+        // (at most D^2 / 1024 compares in a row), then add up in LDS -- the bitonic network's
+        // 21 barrier-separated stages cost more at C1's 64 names
+        __shared__ uint32_t rk[256];
+        if (threadIdx.x < 256) rk[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t P = 4;   // D >= 1: P <= 512
+        while (P < 512 && P * 2 * D <= 1024) P *= 2;
+        const uint32_t v = threadIdx.x / P, part = threadIdx.x % P;
+        if (v < D) {
+            uint32_t y[DICT_W];
+#pragma unroll
+            for (int j = 0; j < DICT_W; ++j) y[j] = (uint32_t)j < nw ? kv[v * nw + j] : 0u;
+            uint32_t cnt = 0;
+            for (uint32_t u = part; u < D; u += P) {
+                uint32_t x[DICT_W];
+#pragma unroll
+                for (int j = 0; j < DICT_W; ++j) x[j] = (uint32_t)j < nw ? kv[u * nw + j] : 0u;
+                // x < y lexicographically, without branches: the first differing word decides
+                bool lt = false, eq = true;
+#pragma unroll
+                for (int j = 0; j < DICT_W; ++j) {
+                    lt = lt || (eq && x[j] < y[j]);
+                    eq = eq && x[j] == y[j];
+                }
+                cnt += lt ? 1u : 0u;
+            }
+            atomicAdd(&rk[v], cnt);
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < D; t += 1024) d.keys[(uint64_t)t * DENT + DICT_W] = rk[t];
+        return;
+    }
     // greater(a, b): pad indices (>= D) sort last
     auto greater = [&](uint32_t a, uint32_t b) -> bool {
         if (a >= D || b >= D) return a >= D && (b < D || a > b);
@@ -278,27 +329,11 @@ __global__ __launch_bounds__(1024) void k_dict_rank(DictRef d) {
     for (uint32_t t = threadIdx.x; t < D; t += 1024) d.keys[(uint64_t)ix[t] * DENT + DICT_W] = t;
 }
 
-// the rank of a row's value (k_compose; the value is in the dictionary unless it is void)
-__device__ __forceinline__ uint32_t dict_rank(const DictRef &d, const uint8_t *p, uint32_t width) {
-    uint32_t k[DICT_W];
-#pragma unroll
-    for (int j = 0; j < DICT_W; ++j) k[j] = (uint32_t)j < d.nw ? be_word(p, width, j) : 0u;
-    const uint32_t h = dict_hash(k, d.nw), tg = h | 2u;
-    uint32_t s = h & d.mask;
-    for (uint32_t probes = 0; probes <= d.mask; ++probes, s = (s + 1) & d.mask) {
-        const uint32_t t = d.slot[2 * s];
-        if (t == 0u) break;
-        if (t == tg) {
-            const uint32_t idx = d.slot[2 * s + 1];
-            if (idx < d.cap) {   // the entry's line: value words and rank
-                const uint4 *e = reinterpret_cast<const uint4 *>(d.keys + (uint64_t)idx * DENT);
-                const uint4 q0 = e[0], q1 = e[1], q2 = e[2];
-                const uint32_t v[DICT_W] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-                if (dict_eq(v, k, d.nw)) return q2.x;
-            }
-        }
-    }
-    return 0u;   // only when the dictionary is void (the host then discards this compose)
+// the rank of slice row r's value (k_compose; garbage only when the dictionary is void, and
+// the host then discards this compose)
+__device__ __forceinline__ uint32_t dict_rank(const DictRef &d, uint64_t r) {
+    const uint32_t idx = d.rowidx[r];
+    return idx < d.cap ? d.keys[(uint64_t)idx * DENT + DICT_W] : 0u;
 }
 
 struct ComposeArgs {
@@ -338,7 +373,7 @@ __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restr
         const uint32_t inv = a.desc[k] ? 0xFFFFFFFFu : 0u;
         const uint8_t *p = a.ptr[k] + (a.direct[k] ? r : src) * a.rstride[k];
         if (a.dict[k]) {
-            words[w * a.stride + i] = dict_rank(a.dref[a.dict[k] - 1], p, a.width[k]) ^ inv;
+            words[w * a.stride + i] = dict_rank(a.dref[a.dict[k] - 1], r) ^ inv;
         } else if (a.kind[k] == IGX_KIND_BYTES) {
             for (uint32_t j = 0; j < nw; ++j) words[(w + j) * a.stride + i] = be_word(p, a.width[k], j) ^ inv;
         } else if (a.kind[k] == IGX_KIND_FLOAT) {
@@ -1725,7 +1760,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     // the ctl words and the slots
     constexpr uint32_t DSLOTS = 2 * DICT_MAXD;
     const size_t dict_ctl_b = igx_align((size_t)DICT_MAXK * 16, 256), dict_slot_b = (size_t)DSLOTS * 8;
-    const size_t dict_val_b = (size_t)DICT_MAXD * DENT * 4;
+    const size_t dict_val_b = (size_t)DICT_MAXD * DENT * 4 + igx_align((size_t)nrows * 4, 256);   // + rowidx
     const size_t dict_clear_b = ndict ? dict_ctl_b + ndict * dict_slot_b : 0;
     const size_t dict_b = ndict ? dict_clear_b + ndict * dict_val_b : 0;
     const size_t sel_b = use_sel ? igx_align((igx_align(limit, 64) + 2 * stride + 64 + SEL_BINS) * 4, 256) : 0;
@@ -1774,6 +1809,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
         d.ctl = dctl + 4 * j;
         d.slot = reinterpret_cast<uint32_t *>(dict_base + dict_ctl_b + j * dict_slot_b);
         d.keys = reinterpret_cast<uint32_t *>(q);
+        d.rowidx = reinterpret_cast<uint32_t *>(q + (size_t)DICT_MAXD * DENT * 4);
         ++j;
         d.nw = keys[k].words;
         d.cap = std::min<uint32_t>(DICT_MAXD, DICT_LDS_WORDS / d.nw);

@@ -458,6 +458,15 @@ def test_string_dictionary_sort(oracle, E, H, torch, monkeypatch):
         want = sel[oracle.go_sort_entries(sub, m, valid=None if valid is None else valid[sel]).astype(np.int64)]
         out = H.host(E.sort_perm(keys_d, n, valid=vd, rowmap=cap, d_count=cnt))[:m]
         assert np.array_equal(out, want), ci
+    # no value to rank: every row nil, and an empty slice (a device count of 0)
+    a = _strings(rng, n, 16, 10)
+    nil = np.zeros(n, np.uint8)
+    got = H.host(E.sort_perm([(H.to_device(a), True)], n, valid=H.to_device(nil)))
+    assert np.array_equal(got, oracle.go_sort_entries([(a, "string", True)], n, valid=nil))
+    cap = torch.zeros((n,), dtype=torch.int32, device="cuda").view(torch.uint32)
+    zero = torch.zeros((1,), dtype=torch.int64, device="cuda").view(torch.uint64)
+    E.sort_perm([(H.to_device(a), False)], n, rowmap=cap, d_count=zero)
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("devplan", [False, True])

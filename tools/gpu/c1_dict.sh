@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/c1_dict
 rm -rf $O; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 100 --timeout-method thread tests/test_gpu_parity.py \
     -k "sort or filter or c1 or topk or ties" > $O/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for rep in 1 2; do
