@@ -28,7 +28,9 @@
 // window holds all but ~1e-4 of the rows.
 // Each lane keeps 8 rows (128 B of loads) in flight per chunk -- the kernel is
 // bound by bytes in flight, not by arithmetic.  Small histograms are replicated per wave
-// to spread LDS atomic contention.  Commit: one HBM atomic add per non-zero counter.
+// to spread LDS atomic contention.  Commit: with one partition and one replica (C3), every
+// workgroup copies its counters and window to HBM as they are and k_hist_reduce adds each
+// bin over the workgroups (two-level); otherwise one HBM atomic add per non-zero counter.
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -61,6 +63,8 @@ struct HistArgs {
     uint32_t ngroups;           // chunk groups (multiple of 8)
     uint64_t divisor;
     uint32_t *hist;
+    uint32_t *partial;          // non-null (one partition, one replica): each workgroup's counters
+    uint32_t *part_lo;          // ... and its window, summed into hist by k_hist_reduce
 };
 
 __host__ __device__ __forceinline__ uint32_t dev_hash(uint32_t d) { return (d * 0x9E3779B1u) >> 24; }
@@ -242,6 +246,12 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
         if (++it % CHUNKS_PER_TILE == 0) __syncthreads();
     }
     __syncthreads();
+    if (a.partial) {   // two-level commit: the counters as they are (one coalesced copy)
+        uint32_t *dst = a.partial + (uint64_t)blockIdx.x * a.rep_words;
+        for (uint32_t i = threadIdx.x; i < a.rep_words; i += TB) dst[i] = h[i];
+        if (threadIdx.x == 0) a.part_lo[blockIdx.x] = lo;
+        return;
+    }
     const uint32_t nkeys = a.ndev * a.ncont;
     const uint32_t kbase = p * a.Kp;
     const uint32_t nkeys_here = kbase < nkeys ? min(a.Kp, nkeys - kbase) : 0u;
@@ -250,6 +260,44 @@ __global__ __launch_bounds__(TB) void k_hist(HistArgs a) {
         for (uint32_t r = 0; r < a.R; ++r) s += (h[r * a.rep_words + (i >> 1)] >> ((i & 1u) * 16u)) & 0xFFFFu;
         if (s) atomicAdd(&a.hist[((uint64_t)kbase + i / a.W) * a.nslots + lo + i % a.W], s);
     }
+}
+
+// The second level of the two-level commit: hist[key][slot] += the workgroups' counters of
+// (key, slot) (each workgroup's window starts at its own lo).  One thread per histogram bin,
+// eight workgroups' words in flight per thread.  The single-level commit -- one HBM atomic
+// per non-zero counter at the end of every workgroup, 1.3M on C3 -- cost 70 us of a 0.42 ms
+// kernel.
+__global__ __launch_bounds__(256) void k_hist_reduce(const uint32_t *__restrict__ partial,
+                                                     const uint32_t *__restrict__ part_lo, uint32_t nb,
+                                                     uint32_t rep_words, uint32_t nkeys, uint32_t W, uint32_t nslots,
+                                                     uint32_t *__restrict__ hist) {
+    __shared__ uint32_t slo[1024];
+    for (uint32_t t = threadIdx.x; t < nb; t += 256) slo[t] = part_lo[t];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (uint64_t)nkeys * nslots) return;
+    const uint32_t key = (uint32_t)(i / nslots), slot = (uint32_t)(i % nslots);
+    uint32_t s = 0;
+    uint32_t g = 0;
+    for (; g + 8 <= nb; g += 8) {
+        uint32_t v[8], ws[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            ws[u] = slot - slo[g + u];
+            const uint32_t b = key * W + min(ws[u], W - 1);
+            v[u] = partial[(uint64_t)(g + u) * rep_words + (b >> 1)] >> ((b & 1u) * 16u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += ws[u] < W ? (v[u] & 0xFFFFu) : 0u;
+    }
+    for (; g < nb; ++g) {
+        const uint32_t ws = slot - slo[g];
+        if (ws < W) {
+            const uint32_t b = key * W + ws;
+            s += (partial[(uint64_t)g * rep_words + (b >> 1)] >> ((b & 1u) * 16u)) & 0xFFFFu;
+        }
+    }
+    if (s) hist[i] += s;
 }
 
 // ig_profio_done's slot per event for the raw hist_key{cmd_flags, dev} form (biolatency.bpf.c:
@@ -328,6 +376,17 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
     a.divisor = divisor;
     a.hist = hist;
     const size_t lds = (size_t)part_bytes * a.R;
+    // one partition, one replica: commit through k_hist_reduce instead of one HBM atomic per
+    // counter (IGX_HIST_ATOMIC_COMMIT=1 keeps the atomics)
+    const bool two_level = a.P == 1 && a.R == 1 && blocks <= 1024 && !std::getenv("IGX_HIST_ATOMIC_COMMIT");
+    if (two_level) {
+        void *sp;
+        const size_t pb = igx_align((size_t)blocks * a.rep_words * 4, 256);
+        const int rc = igx_scratch(ctx, pb + (size_t)blocks * 4, &sp);
+        if (rc) return rc;
+        a.partial = static_cast<uint32_t *>(sp);
+        a.part_lo = reinterpret_cast<uint32_t *>(static_cast<char *>(sp) + pb);
+    }
     const bool vec = (reinterpret_cast<uintptr_t>(dev) | reinterpret_cast<uintptr_t>(cont) |
                       reinterpret_cast<uintptr_t>(delta)) % 16 == 0 && (dev || a.single);
     // the vector path loads dev unconditionally: single-key mode without a column scalar-loads
@@ -336,6 +395,11 @@ int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont, co
     else if (divisor == 1000000) launch<1000000>(a, blocks, lds, ctx->stream, use_vec);
     else if (divisor == 1) launch<1>(a, blocks, lds, ctx->stream, use_vec);
     else launch<0>(a, blocks, lds, ctx->stream, use_vec);
+    if (two_level) {
+        const uint64_t bins = nkeys * nslots;
+        hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((bins + 255) / 256)), dim3(256), 0, ctx->stream, a.partial,
+                           a.part_lo, blocks, a.rep_words, (uint32_t)nkeys, a.W, nslots, hist);
+    }
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }

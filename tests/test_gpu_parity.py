@@ -400,14 +400,16 @@ def test_device_planned_sort_matches_host_planned(oracle, E, H, torch, monkeypat
 
 
 def _strings(rng, n, width, distinct):
-    """n strings of `width` (>= 8) bytes drawn from exactly `distinct` values over a 3-letter
-    alphabet (long shared prefixes), of every length from 8 to the field (zero padded, as Go
-    compares them), plus the empty string.  A value's last 8 letters are its index in base 3."""
+    """n strings of `width` bytes drawn from exactly `distinct` values over a 3-letter alphabet
+    (long shared prefixes), of every length from D = min(8, width) to the field (zero padded, as
+    Go compares them), plus the empty string.  A value's last D letters are its index in base 3."""
+    D = min(8, width)
+    assert distinct <= 3 ** D
     pool = np.zeros((distinct, width), np.uint8)
     for v in range(1, distinct):
-        ln = int(rng.integers(8, width + 1))
-        pool[v, :ln - 8] = rng.integers(97, 100, ln - 8)
-        pool[v, ln - 8:ln] = [97 + (v // 3 ** d) % 3 for d in range(7, -1, -1)]
+        ln = int(rng.integers(D, width + 1))
+        pool[v, :ln - D] = rng.integers(97, 100, ln - D)
+        pool[v, ln - D:ln] = [97 + (v // 3 ** d) % 3 for d in range(D - 1, -1, -1)]
     assert len(np.unique(pool, axis=0)) == distinct
     return pool[rng.integers(0, distinct, n)]
 
@@ -416,8 +418,8 @@ def test_string_dictionary_sort(oracle, E, H, torch, monkeypatch):
     """String keys of many rows sort through a dictionary of their distinct values (k_dict_*:
     the rank replaces the bytes, one or two live digits instead of one per byte); a dictionary
     over capacity (4 096 values of <= 16 bytes, 2 048 of 32) is void and the raw bytes are
-    composed instead.  Same order as IGX_SORT_DICT=0 and as Go's SliceStable restatement: 8-, 12-,
-    16- and 32-byte strings, ascending and descending, with ties broken by position, nil rows, a
+    composed instead.  Same order as IGX_SORT_DICT=0 and as Go's SliceStable restatement: 6-, 8-,
+    12-, 16-, 20- and 32-byte strings, ascending and descending, with ties broken by position, nil rows, a
     selection vector with a device count, and exactly-at-capacity / over-capacity value counts."""
     rng = np.random.default_rng(5)
     n = 150_000
@@ -428,6 +430,7 @@ def test_string_dictionary_sort(oracle, E, H, torch, monkeypatch):
         [(8, 5000, True), (32, 2000, False)],                 # void (8-byte) + valid (32-byte)
         [(12, 300, True), (32, 2049, True), ("int64", None, True)],   # the 32-byte one over capacity
         [(32, 1, False), (16, 3, True)],                      # constant strings
+        [(6, 500, False), (20, 700, True), ("uint16", None, False)],   # 2 and 5 words, partial last words
     ]
     for ci, spec in enumerate(cases):
         keys_d, keys_o = [], []
