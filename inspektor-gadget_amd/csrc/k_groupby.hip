@@ -1441,13 +1441,19 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     }
 
     __syncthreads();
+    // the cache's sums: one lane per (entry, aggregate), so an entry's adds leave from adjacent
+    // lanes of one instruction into its value record -- one memory-side request per record (the
+    // update ring's shape) instead of one per aggregate from a lane that owns the entry
+    const uint32_t na = a.naggs;
+    for (uint32_t q = threadIdx.x; q < E * na; q += GTB) {
+        const uint32_t e = q / na, x = q - e * na;
+        const uint32_t gs = c.st[e];
+        const uint64_t s = gs < ST_BUSY ? c.agg[x * E + e] : 0ull;
+        if (s) gadd(rec_agg(a, gs, (int)x), (unsigned long long)s);
+    }
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         const uint32_t gs = c.st[e];
         if (gs >= ST_BUSY) continue;
-        for (uint32_t x = 0; x < a.naggs; ++x) {
-            const uint64_t s = c.agg[x * E + e];
-            if (s) gadd(rec_agg(a, gs, (int)x), (unsigned long long)s);
-        }
         const uint64_t f = c.first[e];
         const uint64_t fi = (ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
                                                                          koff_of(KW) + 8)) & READY_IDX) - 1;
