@@ -1461,6 +1461,56 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     }
 }
 
+// ---- AUTO's re-probe: the cached form's LDS miss share, estimated ---------------------------
+// After a run of partitioned intervals AUTO asks whether the stream has turned skewed enough for
+// the cached form.  Running a whole interval cached to find out cost C4 7.6 ms against 3.0; the
+// probe interval now runs partitioned, and this kernel replays the cache's admission on a sample
+// of the rows: the cached kernel's per-workgroup row interleaving, its E-entry 8-way sets and
+// its second-miss ghost filter, on the key hash alone (a tag match counts as a hit; no HBM slot,
+// no sums).  Its misses go to the error block's miss word, which the cached kernel would have
+// written; fin_apply scales them to the interval.
+template <class L, int NA>
+__global__ __launch_bounds__(GTB) void k_gb_estimate(GbArgs a, uint64_t nsample) {
+    constexpr int KW = L::KW;
+    extern __shared__ uint64_t lds[];
+    LdsCache<KW> c{};
+    c.E = a.lds_entries;
+    c.nsets = a.lds_entries / 8;
+    c.tag = reinterpret_cast<uint32_t *>(lds);
+    c.ghost = c.tag + c.E;
+    for (uint32_t e = threadIdx.x; e < c.E; e += GTB) c.tag[e] = 0;
+    for (uint32_t e = threadIdx.x; e < GHOST; e += GTB) c.ghost[e] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t n = min(a.n, nsample);
+    const uint64_t stride = (uint64_t)gridDim.x * GTB;
+    uint32_t nmiss = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * GTB + wave * 64; base < n; base += stride) {
+        const uint64_t row = base + lane;
+        RowRaw<L, NA> R;
+        issue_row<L, NA>(a, min(row, n - 1), R);
+        uint32_t k[KW];
+        uint64_t v[NA];
+        if (!(decode_row<L, NA>(a, row, R, k, v) && row < n)) continue;
+        const uint64_t h = hash_key<KW>(k);
+        const uint32_t sb = lds_set(c, h), t = lds_tag(h);
+        uint32_t tg[8];
+        lds_tags(c, sb, tg);
+        bool hit = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hit = hit || tg[j] == t;
+        if (hit) continue;
+        ++nmiss;
+        if (!ghost_admit<KW>(a, c, h)) continue;
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m |= (tg[j] == 0 ? 1u : 0u) << j;
+        if (m) (void)atomicCAS(&c.tag[sb + (uint32_t)(__builtin_ffs((int)m) - 1)], 0u, t);
+    }
+    for (int o = 32; o > 0; o >>= 1) nmiss += __shfl_xor(nmiss, o);
+    if (lane == 0 && nmiss) atomicAdd(reinterpret_cast<unsigned long long *>(a.err + 2), (unsigned long long)nmiss);
+}
+
 // ---- direct form: no LDS cache ---------------------------------------------------------
 // For near-uniform, high-cardinality streams (C4's distinct tuples: nearly every row misses
 // any per-CU cache) the LDS cache, its rings and its roles only add work: every row goes
@@ -1746,8 +1796,11 @@ struct igx_table {
     // may be collected after the next interval's reset and updates changed the live fields
     struct {
         uint64_t rows_fed;
-        bool direct, part, region;
+        bool direct, part, region, probe;
+        uint64_t sampled;   // probe: rows the estimator replayed
     } fin_snap{};
+    bool interval_probe = false;   // AUTO: the last partitioned interval of a run (k_gb_estimate)
+    uint64_t probe_rows = 0;       // ... the rows its estimator replayed
     unsigned long long *dbg_cnt = nullptr;
     uint8_t *text[32] = {};      // IP text of the groups, per IGX_TSRC_IPTEXT sort key
     uint64_t text_rows[32] = {};
@@ -1949,6 +2002,24 @@ static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     a.lds_entries = E;
     const size_t lds = E * entry + rings;
     hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), lds, ctx->stream, a);
+}
+
+// k_gb_estimate with the cached kernel's geometry (its E and its GHOST filter)
+constexpr uint64_t PROBE_ROWS = 16u << 20;   // rows the re-probe replays (C4: 16M of 125M)
+template <class L, int NA>
+static void launch_estimate_as(igx_ctx *ctx, GbArgs a, uint32_t blocks, uint64_t nsample) {
+    const size_t entry = 4 + 4 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
+    const size_t rings = ARING * 16 + MRING * (16 * MissRing<L::KW, NA>::EQ + 4) + GHOST * 4;
+    const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, (GB_LDS_TOTAL - rings) / (8 * entry)));
+    a.lds_entries = 8 * nsets;
+    a.admit_mask = std::max<uint32_t>(a.admit_mask, 1u);
+    const size_t lds = ((size_t)a.lds_entries + GHOST) * 4;
+    hipLaunchKernelGGL((k_gb_estimate<L, NA>), dim3(blocks), dim3(GTB), lds, ctx->stream, a, nsample);
+}
+template <class L>
+static void launch_estimate(igx_ctx *ctx, const GbArgs &a, uint32_t blocks, uint64_t nsample) {
+    if (a.naggs <= 2) launch_estimate_as<L, 2>(ctx, a, blocks, nsample);
+    else launch_estimate_as<L, AMAX>(ctx, a, blocks, nsample);
 }
 
 // The diagnostic variants (IGX_GB_DEBUG) are compiled for the top-tcp key only, so the
@@ -2263,6 +2334,10 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
 // one update over layout L in the interval's form
 template <class L>
 static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
+    if (t->interval_part && t->interval_probe && t->rows_fed == a.n) {
+        t->probe_rows = std::min<uint64_t>(a.n, PROBE_ROWS);
+        launch_estimate<L>(ctx, a, blocks, t->probe_rows);
+    }
     if (t->interval_part) {
         const GbArgs saved = a;   // launch_part turns the fused predicates into a row mask
         const int rc = launch_part<L>(t, ctx, a);
@@ -2271,7 +2346,10 @@ static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
         // update runs cached instead (the forms share the table protocol, so they may mix
         // within an interval), and AUTO measures again at the next interval
         (void)hipGetLastError();
+        if (t->interval_probe)   // the cached kernel measures this interval itself: drop the estimate
+            IGX_HIP(ctx, hipMemsetAsync(t->err + 2, 0, 8, ctx->stream));
         t->interval_part = false;
+        t->interval_probe = false;
         t->direct_left = 0;
         a = saved;
     }
@@ -2535,7 +2613,9 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     if (t->rows_fed == nrows) {
         t->interval_direct = t->mode == IGX_GB_DIRECT;
         t->interval_part = t->mode == IGX_GB_PART || (t->mode == IGX_GB_AUTO && t->direct_left > 0);
-        if (t->mode == IGX_GB_AUTO && t->direct_left > 0) --t->direct_left;
+        t->interval_probe = false;
+        t->probe_rows = 0;
+        if (t->mode == IGX_GB_AUTO && t->direct_left > 0) t->interval_probe = --t->direct_left == 0;
         t->interval_region = false;
         if (t->region_off > 0) --t->region_off;
     }
@@ -2592,6 +2672,8 @@ static int fin_launch(igx_table *t) {
     t->fin_snap.direct = t->interval_direct;
     t->fin_snap.part = t->interval_part;
     t->fin_snap.region = t->interval_region;
+    t->fin_snap.probe = t->interval_part && t->interval_probe;
+    t->fin_snap.sampled = t->probe_rows;
     if (tiles <= SLOTS_INLINE_TILES) {
         hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                            (const uint32_t *)nullptr, t->tile_cnt, t->groups, t->n_groups, t->err, t->fin_dev, seq);
@@ -2636,13 +2718,19 @@ static int fin_apply(igx_table *t) {
     // go faster with the state-machine probers; hit-heavy ones with the batch probers.  When
     // nearly every row missed, the cache is pure overhead: AUTO runs the next DIRECT_RUN
     // intervals in the partitioned form (streamed passes instead of a random HBM probe per
-    // row; C4: 4.1 vs 4.4 ms direct, 6.4 ms cached), then one cached interval to measure again.
+    // row; C4: 4.1 vs 4.4 ms direct, 6.4 ms cached); the last of them re-probes the stream with
+    // k_gb_estimate on a sample, and only a stream that has stopped missing goes cached again.
     if (f.rows_fed >= 1000000 && !f.direct && !f.part) {
         t->prefer_sm = misses * 10 > f.rows_fed * 7;
         t->miss_pm = (uint32_t)(misses * 1000 / f.rows_fed);
         t->more_probers = t->miss_pm > (t->more_probers ? MORE_PROBERS_OFF_PM : MORE_PROBERS_ON_PM);
         if (t->mode == IGX_GB_AUTO && misses * 100 > f.rows_fed * DIRECT_MISS_PCT) t->direct_left = DIRECT_RUN;
     }
+    // the probe interval (partitioned, with k_gb_estimate on a sample): still nearly all misses
+    // -> another run of partitioned intervals; otherwise the next interval runs cached and
+    // measures the stream itself
+    if (f.probe && f.sampled && t->mode == IGX_GB_AUTO && misses * 100 > f.sampled * DIRECT_MISS_PCT)
+        t->direct_left = DIRECT_RUN;
     if (err) return igx_fail(ctx, IGX_ENOSPC, "groupby: table full or probe failure (err=%u)", err);
     if (ng > t->cap)
         return igx_fail(ctx, IGX_ENOSPC, "groupby: %llu distinct keys exceed capacity %llu",

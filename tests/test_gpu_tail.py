@@ -164,3 +164,40 @@ def test_auto_region_overflow_async_pipeline(E, H, igx):
     assert any(f["form"] == A.GB_PART and not f["region"] for f in later), forms
     tab.destroy()
 
+
+
+def test_auto_reprobe_by_estimate(E, H, igx, oracle):
+    """AUTO's re-probe: after a near-uniform stream sends a table to the partitioned form, the
+    last interval of each partitioned run replays the LDS cache on a sample (k_gb_estimate)
+    instead of running a whole interval cached -- a stream that still misses stays partitioned
+    with no cached interval in between; once the stream turns skewed, the probe sends the next
+    interval to the cached form.  Every interval's groups and counts exact."""
+    A = igx._abi
+    rng = np.random.default_rng(9)
+    n = 4_000_000
+    uni = rng.integers(1, 20_000_000, n, dtype=np.uint32)
+    cdf = oracle.zipf_cdf(2000, 1.2)
+    skew = (np.searchsorted(cdf, rng.random(n)) + 1).astype(np.uint32)
+    tab = E.Table([4], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], 8_000_000)
+
+    def interval(kd, uk, cnt):
+        tab.reset()
+        tab.update([kd], [0], n, 0)
+        f = tab.info()
+        fin = tab.finalize()
+        assert fin["n_groups"] == len(uk)
+        row = H.host(tab.gather(tab.sort([(A.TSRC_AGG, 0, True)], 1)))[0]
+        o = fin["key_bytes"]
+        assert row[o:o + 8].view(np.uint64)[0] == cnt.max()
+        return f
+
+    kd, (uk, cnt) = H.to_device(uni), np.unique(uni, return_counts=True)
+    forms = [interval(kd, uk, cnt) for _ in range(40)]
+    assert forms[0]["form"] == A.GB_CACHED
+    assert all(f["form"] == A.GB_PART for f in forms[1:]), [f["form"] for f in forms]
+    kd, (uk, cnt) = H.to_device(skew), np.unique(skew, return_counts=True)
+    forms = [interval(kd, uk, cnt) for _ in range(20)]
+    cached = [i for i, f in enumerate(forms) if f["form"] == A.GB_CACHED]
+    assert cached and cached[0] <= 17, [f["form"] for f in forms]   # within one partitioned run
+    assert all(f["form"] == A.GB_CACHED for f in forms[cached[0]:]), [f["form"] for f in forms]
+    tab.destroy()
