@@ -530,3 +530,34 @@ def test_hist_slot_boundaries(oracle, E, H, torch, divisor):
     contc = H.to_device(np.zeros(n, np.uint32))
     got = H.host(E.hist_log2(devc, contc, d, [7], 1, divisor=divisor))          # 16-B loads
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n", [1_000_003, 16_777_217])
+def test_filter_int_mark_and_both_compactions(oracle, E, H, igx, torch, n):
+    """igx_filter on integer predicates (the kernel that loads every row's values before it
+    compares: signed and unsigned, 1/2/4/8-byte columns, a negated predicate, nil rows) and
+    both compactions: up to 16M rows the compaction sums its tile's predecessors itself, above
+    that the scan kernel runs first.  Same row ids as numpy, in input order."""
+    import ctypes as C
+    A = igx._abi
+    rng = np.random.default_rng(n)
+    i8 = rng.integers(-100, 100, n, dtype=np.int8)
+    u16 = rng.integers(0, 60000, n, dtype=np.uint16)
+    i32 = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+    i64 = rng.integers(-2**40, 2**40, n, dtype=np.int64)
+    valid = (rng.random(n) < 0.97).astype(np.uint8)
+
+    def pred(col, cmp, value, dtype, negate=False):
+        b = np.array([value], dtype=dtype).view(np.uint8)
+        return A.Pred(col, cmp, int(negate), len(b), (C.c_uint8 * A.MAX_REF)(*b.tolist()))
+
+    cols = [H.to_device(a) for a in (i8, u16, i32, i64)]
+    preds = [pred(0, A.CMP_GE, -20, np.int8), pred(1, A.CMP_LT, 45000, np.uint16),
+             pred(2, A.CMP_GT, -2**30, np.int32), pred(3, A.CMP_LE, 2**39, np.int64, negate=True)]
+    got = H.host(E.filter_rows(cols, preds, n, valid=H.to_device(valid))).astype(np.int64)
+    want = np.flatnonzero((i8 >= -20) & (u16 < 45000) & (i32 > -2**30) & ~(i64 <= 2**39) & (valid != 0))
+    assert np.array_equal(got, want)
+    # MatchAny over the same predicates, no nil mask
+    got = H.host(E.filter_rows(cols, preds, n, any=True)).astype(np.int64)
+    want = np.flatnonzero((i8 >= -20) | (u16 < 45000) | (i32 > -2**30) | ~(i64 <= 2**39))
+    assert np.array_equal(got, want)
