@@ -2,7 +2,8 @@
 the time goes.  Not part of the product path or the tests.
 
     python tools/ablate_groupby.py --events 100000000 --keys 1000000 --zipf 1.1
-Variants (IGX_GB_DEBUG bits, read per launch): 0 full, 1 load+hash only, 2 stop after the
+    python tools/ablate_groupby.py --layout file --events 125000000 --keys 10000000 --zipf 1.05 --variants 0
+Variants (IGX_GB_DEBUG bits, read per launch; the top-file key only in an IGX_GB_DEBUG_FILE build): 0 full, 1 load+hash only, 2 stop after the
 LDS lookup (misses dropped), 4 no HBM atomics on misses, 8 full + hit/miss counters.
 """
 import argparse
@@ -26,6 +27,7 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--variants", default="0,1,2,4,8")
     p.add_argument("--noreset", action="store_true", help="keep the table between launches (no new keys after the first)")
+    p.add_argument("--layout", choices=("tcp", "file"), default="tcp")
     a = p.parse_args()
     variants = [int(x) for x in a.variants.split(",")]
     import torch
@@ -34,11 +36,19 @@ def main():
     E, H, A = igx.engine, igx.columns, igx._abi
     N, G = a.events, a.keys
     cdf = H.to_device(O.zipf_cdf(G, a.zipf))
-    ev = E.gen_tcp(0xC2, 0, G, cdf, 0, N)
-    names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
-    cols = [ev[k] for k in names]
-    tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2],
-                  [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)], G + G // 4)
+    if a.layout == "tcp":
+        ev = E.gen_tcp(0xC2, 0, G, cdf, 0, N)
+        names = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
+        cols = [ev[k] for k in names]
+        tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2],
+                      [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)], G + G // 4)
+        nkey = 8
+    else:   # bench.py's C5: file_id key, reads / rbytes / writes / wbytes
+        bench = importlib.import_module("bench")
+        ev = E.gen_file(0xC5, 0, G, cdf, 0, N)
+        cols = [ev[k] for k in bench.C5_NAMES]
+        tab = E.Table(bench.C5_WIDTHS, bench.c5_aggs(A), G + G // 4)
+        nkey = 4
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {}
     for r in range(a.rounds):
@@ -47,9 +57,9 @@ def main():
             if not a.noreset:
                 tab.reset()
             elif r == 0 and v == variants[0]:
-                tab.update(cols, list(range(8)), N, 0)   # populate: later launches find every key
+                tab.update(cols, list(range(nkey)), N, 0)   # populate: later launches find every key
             e0.record()
-            tab.update(cols, list(range(8)), N, 0)
+            tab.update(cols, list(range(nkey)), N, 0)
             e1.record()
             torch.cuda.synchronize()
             res.setdefault(v, []).append(e0.elapsed_time(e1))
@@ -62,7 +72,7 @@ def main():
                     res.setdefault("waits_lfull_pempty_ufull_sidle", []).append([cnt[4], cnt[5], cnt[6], cnt[7]])
     os.environ.pop("IGX_GB_DEBUG", None)
     out = {str(k): (float(np.median(v)) if not isinstance(k, str) else v[-1]) for k, v in res.items()}
-    out.update({"events": N, "keys": G, "zipf": a.zipf})
+    out.update({"events": N, "keys": G, "zipf": a.zipf, "layout": a.layout, "noreset": a.noreset})
     print(json.dumps(out))
     tab.destroy()
 
