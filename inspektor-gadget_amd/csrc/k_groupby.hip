@@ -1137,7 +1137,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
 // instruction's adjacent 16-B pieces: one write-through request per 64 B, instead of a request
 // per 16-B store of a lane writing its record alone (C5: 5 of a claim's 8 requests, C2: 7 of 10).
 // Ends with s_waitcnt vmcnt(0): the records are visible before the claimers publish `ready`.
-template <int KW, int NA>
+template <int KW, int NA, bool WAIT = true>
 __device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, uint32_t s, const uint32_t (&k)[KW],
                                                  uint64_t tag, uint64_t gidx, const uint64_t (&v)[NA]) {
     constexpr uint32_t KOFF = koff_of(KW);
@@ -1198,13 +1198,16 @@ __device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, ui
         }
         for (uint32_t i = 0; i < RPI && todo; ++i) todo &= todo - 1;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // The batch prober: a wave takes 64 cells of the miss ring and resolves them together, one
 // round trip per round: every unresolved lane reads its current slot's record; a lane that
 // finds it empty claims it (CAS), and the round's claims are written cooperatively
-// (claim_store_coop) and published before the next round.  A lane that meets its own tag
+// (claim_store_coop) and published (`ready`, then the occupancy bit) at the top of the next
+// round -- which waits for its probe loads anyway -- or, when the batch is resolved, before the
+// wave takes its next cells, so the stores overlap the LDS adoption and ring pushes instead of
+// a wait of their own.  A lane that meets its own tag
 // not yet published -- possibly claimed by a lane of this very wave -- reads it again next
 // round instead of spinning.  Resolved misses then adopt a free LDS entry or go to the
 // HBM-update ring.
@@ -1214,7 +1217,25 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
+    // a claim written but not yet published: its slot (SLOT_OVF: none) and event index
+    uint32_t pend_s[PB];
+    uint64_t pend_g[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) pend_s[j] = SLOT_OVF;
+    auto publish = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the claims' key / value stores
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            if (pend_s[j] != SLOT_OVF) {
+                st_agent(reinterpret_cast<uint64_t *>(a.krec + (uint64_t)pend_s[j] * a.krec_len + KOFF + 8),
+                         (a.ep << 48) | (pend_g[j] + 1));
+                atomicOr(a.occ + (pend_s[j] >> 5), 1u << (pend_s[j] & 31));
+                pend_s[j] = SLOT_OVF;
+            }
+        }
+    };
     for (;;) {
+        publish();   // the previous batch's last claims (their stores overlapped its LDS work)
         uint32_t claim = 0;
         if (lane == 0) claim = atomicAdd(&m.ctl[1], 64u * PB);
         claim = __shfl(claim, 0);
@@ -1277,6 +1298,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
 #pragma unroll
             for (int j = 0; j < PB; ++j) more = more || act[j];
             if (!__ballot(more)) break;
+            publish();   // waits for this round's probe loads, which it needs anyway
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 const uint64_t tag = (x[j].h & ~EP_MAX) | a.ep;
@@ -1334,11 +1356,10 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                     }
                 }
                 if (__ballot(won)) {
-                    claim_store_coop<KW, NA>(a, won, (uint32_t)s[j], x[j].k, tag, x[j].gidx, x[j].v);
-                    if (won) {
-                        st_agent(reinterpret_cast<uint64_t *>(a.krec + s[j] * a.krec_len + KOFF + 8),
-                                 (a.ep << 48) | (x[j].gidx + 1));
-                        atomicOr(a.occ + (s[j] >> 5), 1u << (s[j] & 31));
+                    claim_store_coop<KW, NA, false>(a, won, (uint32_t)s[j], x[j].k, tag, x[j].gidx, x[j].v);
+                    if (won) {   // published by the next publish() (next round or next batch)
+                        pend_s[j] = (uint32_t)s[j];
+                        pend_g[j] = x[j].gidx;
                         first_ins[j] = x[j].gidx;
                         claimed[j] = true;
                     }
