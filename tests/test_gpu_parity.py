@@ -461,6 +461,14 @@ def test_string_dictionary_sort(oracle, E, H, torch, monkeypatch):
         want = sel[oracle.go_sort_entries(sub, m, valid=None if valid is None else valid[sel]).astype(np.int64)]
         out = H.host(E.sort_perm(keys_d, n, valid=vd, rowmap=cap, d_count=cnt))[:m]
         assert np.array_equal(out, want), ci
+    # high bytes (>= 0x80) compare unsigned, as Go's string comparison does: 900 distinct
+    # 16-byte values of random bytes 1..255 (no NUL), two sort directions
+    pool = rng.integers(1, 256, (900, 16), dtype=np.uint8)
+    pool[::7, 8:] = 0                                       # shorter values, zero padded
+    a = pool[rng.integers(0, 900, n)]
+    for desc in (False, True):
+        got = H.host(E.sort_perm([(H.to_device(a), desc)], n))
+        assert np.array_equal(got, oracle.go_sort_entries([(a, "string", desc)], n)), desc
     # no value to rank: every row nil, and an empty slice (a device count of 0)
     a = _strings(rng, n, 16, 10)
     nil = np.zeros(n, np.uint8)
