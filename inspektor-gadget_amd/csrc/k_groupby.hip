@@ -148,7 +148,10 @@ struct GbArgs {
     uint32_t vrec_words;    // VR / 8
     uint32_t vrec_total;    // S x VR when below 4 GiB (16-B buffer stores of a claim), else 0
     uint32_t *err;
-    uint32_t *occ;          // occupancy bitmap, one bit per slot (set by the claimer)
+    uint32_t *occ;          // occupancy bitmap, one bit per slot (set by the partitioned form's claimers)
+    uint8_t *occb;          // occupancy byte map, one byte per slot: the cached form's claimers store
+                            // 1 with a plain byte store (no atomic: one claimer per slot), finalize
+                            // folds it into the bitmap (k_slots_count)
     uint64_t ep;            // the interval's epoch (1..EP_MAX): tags and `ready` of older
                             // epochs read as empty
     uint64_t rmask;         // probe region slots - 1 (probing wraps inside a region)
@@ -1068,7 +1071,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
         // 4. publish the records claimed last iteration (their stores are now complete)
         if (st == PUB) {
             st_agent(reinterpret_cast<uint64_t *>(rec + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
-            atomicOr(a.occ + (s >> 5), 1u << (s & 31));
+            a.occb[s] = 1;
             finish_miss<KW, NA, DBG>(a, c, r, x, s, x.gidx, true);
             st = FREE;
         }
@@ -1204,7 +1207,7 @@ __device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, ui
 // The batch prober: a wave takes 64 cells of the miss ring and resolves them together, one
 // round trip per round: every unresolved lane reads its current slot's record; a lane that
 // finds it empty claims it (CAS), and the round's claims are written cooperatively
-// (claim_store_coop) and published (`ready`, then the occupancy bit) at the top of the next
+// (claim_store_coop) and published (`ready`, then the occupancy byte) at the top of the next
 // round -- which waits for its probe loads anyway -- or, when the batch is resolved, before the
 // wave takes its next cells, so the stores overlap the LDS adoption and ring pushes instead of
 // a wait of their own.  A lane that meets its own tag
@@ -1229,7 +1232,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
             if (pend_s[j] != SLOT_OVF) {
                 st_agent(reinterpret_cast<uint64_t *>(a.krec + (uint64_t)pend_s[j] * a.krec_len + KOFF + 8),
                          (a.ep << 48) | (pend_g[j] + 1));
-                atomicOr(a.occ + (pend_s[j] >> 5), 1u << (pend_s[j] & 31));
+                a.occb[pend_s[j]] = 1;
                 pend_s[j] = SLOT_OVF;
             }
         }
@@ -1610,11 +1613,31 @@ __global__ __launch_bounds__(256) void k_occ_from_tags(const uint8_t *__restrict
     occ[w] |= m;   // OR: earlier cached updates of the interval may have set bits already
 }
 
-__global__ __launch_bounds__(256) void k_slots_count(const uint32_t *__restrict__ occ, uint64_t nwords,
-                                                     uint32_t *__restrict__ cnt) {
+// 4 bytes of the byte map (each 0 or 1) -> 4 bits, byte j -> bit j
+__device__ __forceinline__ uint32_t byte_bits(uint32_t w) { return (w | (w >> 7) | (w >> 14) | (w >> 21)) & 0xFu; }
+
+// per-tile counts of occupied slots; with occb, first folds the byte map's 32 bytes of each
+// bitmap word into it and clears them (the byte map is left zero for the next interval)
+__global__ __launch_bounds__(256) void k_slots_count(uint32_t *__restrict__ occ, uint64_t nwords,
+                                                     uint32_t *__restrict__ cnt, uint8_t *__restrict__ occb) {
     __shared__ uint32_t wc[4];
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t c = i < nwords ? (uint32_t)__popc(occ[i]) : 0u;
+    uint32_t m = i < nwords ? occ[i] : 0u;
+    if (occb && i < nwords) {
+        uint4 *b = reinterpret_cast<uint4 *>(occb) + 2 * i;
+        const uint4 b0 = b[0], b1 = b[1];
+        const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint32_t f = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f |= byte_bits(w[j]) << (4 * j);
+        if (f) {
+            m |= f;
+            occ[i] = m;
+            b[0] = make_uint4(0, 0, 0, 0);
+            b[1] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    uint32_t c = (uint32_t)__popc(m);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
@@ -1714,12 +1737,15 @@ __global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict_
     }
 }
 
-// an interval's reset: the occupancy bitmap and the error block in one launch
+// an interval's reset: the occupancy bitmap and the error block in one launch, and the byte
+// map when claims since the last finalize left bytes in it (nb16 of its 16-B quads, else 0)
 __global__ __launch_bounds__(256) void k_reset_clear(uint32_t *__restrict__ occ, uint64_t nwords,
-                                                     uint32_t *__restrict__ err) {
+                                                     uint32_t *__restrict__ err, uint4 *__restrict__ occb,
+                                                     uint64_t nb16) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t n4 = nwords / 4;
     for (uint64_t q = i; q < n4; q += (uint64_t)gridDim.x * 256) reinterpret_cast<uint4 *>(occ)[q] = make_uint4(0, 0, 0, 0);
+    for (uint64_t q = i; q < nb16; q += (uint64_t)gridDim.x * 256) occb[q] = make_uint4(0, 0, 0, 0);
     if (i < (nwords & 3)) occ[n4 * 4 + i] = 0;
     if (i < 4) err[i] = 0;
 }
@@ -1786,6 +1812,8 @@ struct igx_table {
     uint32_t *groups = nullptr;  // occupied slots after finalize
     uint32_t *tile_cnt = nullptr;
     uint32_t *occ = nullptr;     // occupancy bitmap (nslots bits)
+    uint8_t *occb = nullptr;     // occupancy byte map (32 x occ_words bytes)
+    bool occb_dirty = false;     // cached-form claims since the byte map was last folded / cleared
     uint64_t occ_words = 0;
     uint64_t ep = 0;             // current epoch (1..EP_MAX)
     uint64_t *n_groups = nullptr;
@@ -1926,6 +1954,8 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
     t->occ_words = (ns + 31) / 32;
     if (e == hipSuccess) e = hipMalloc(&t->occ, t->occ_words * 4);
+    if (e == hipSuccess) e = hipMalloc(&t->occb, t->occ_words * 32);
+    if (e == hipSuccess) e = hipMemsetAsync(t->occb, 0, t->occ_words * 32, ctx->stream);
     if (e == hipSuccess) t->n_groups = reinterpret_cast<uint64_t *>(t->err + 4);   // behind the error block
     if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
     if (e == hipSuccess)
@@ -1969,9 +1999,11 @@ extern "C" int igx_groupby_reset(igx_table *t) {
         IGX_HIP(ctx, hipGetLastError());
         t->ep = 1;
     }
-    // the bitmap, the error bits and the LDS-miss count
-    hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)std::min<uint64_t>(1024, (t->occ_words / 4 + 255) / 256 + 1)), dim3(256),
-                       0, ctx->stream, t->occ, t->occ_words, t->err);
+    // the bitmap, the error bits and the LDS-miss count (and the byte map if it holds claims)
+    const uint64_t nb16 = t->occb_dirty ? t->occ_words * 2 : 0;
+    hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)std::min<uint64_t>(1024, (std::max(t->occ_words / 4, nb16) + 255) / 256 + 1)),
+                       dim3(256), 0, ctx->stream, t->occ, t->occ_words, t->err, reinterpret_cast<uint4 *>(t->occb), nb16);
+    t->occb_dirty = false;
     IGX_HIP(ctx, hipGetLastError());
     t->rows_fed = 0;
     t->host_groups = 0;
@@ -1987,6 +2019,7 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->groups);
     (void)hipFree(t->tile_cnt);
     (void)hipFree(t->occ);
+    (void)hipFree(t->occb);
     (void)hipFree(t->dbg_cnt);
     (void)hipFree(t->p_recs);
     (void)hipFree(t->p_cnt);
@@ -2374,8 +2407,12 @@ static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
         t->direct_left = 0;
         a = saved;
     }
-    if (t->interval_direct) launch_direct<L>(ctx, a);
-    else launch_gb<L>(ctx, a, blocks);
+    if (t->interval_direct) {
+        launch_direct<L>(ctx, a);
+    } else {
+        t->occb_dirty = true;   // the cached form's claims mark the byte map
+        launch_gb<L>(ctx, a, blocks);
+    }
     return IGX_OK;
 }
 
@@ -2606,6 +2643,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.vrec_total = t->nslots * t->vrec_len < (1ull << 32) ? (uint32_t)(t->nslots * t->vrec_len) : 0u;
     a.err = t->err;
     a.occ = t->occ;
+    a.occb = t->occb;
     a.ep = t->ep;
     a.sshift = 64 - t->sbits;
     a.rmask = (1ull << t->rbits) - 1;
@@ -2686,7 +2724,8 @@ static int fin_launch(igx_table *t) {
         hipLaunchKernelGGL(k_occ_from_tags, dim3((unsigned)((t->occ_words + 255) / 256)), dim3(256), 0, ctx->stream,
                            t->krec, t->krec_len, t->koff, t->nslots, t->ep, t->occ);
     hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
-                       t->tile_cnt);
+                       t->tile_cnt, t->occb_dirty ? t->occb : (uint8_t *)nullptr);
+    t->occb_dirty = false;
     // the kernel that finds the group count also writes the read-back into fin_host
     const uint64_t seq = ++t->fin_seq;
     t->fin_snap.rows_fed = t->rows_fed;

@@ -200,6 +200,45 @@ def test_intervals_and_epoch_wrap(oracle, E, H, igx, torch):
     tab.destroy()
 
 
+def test_occupancy_across_finalize_reset_and_forms(oracle, E, H, igx, torch):
+    """The cached form marks its claims in the occupancy byte map, which finalize folds into
+    the bitmap (and clears) and reset clears when no finalize did: a reset with no finalize
+    drops the interval's groups; updates after a finalize add to them; an interval of the
+    cached form then one of the partitioned and one of the direct form list exactly their
+    own groups."""
+    A = igx._abi
+    n = 200_000
+    evs = []
+    for seed, G in ((0xA7, 20_000), (0xB8, 30_000)):
+        ev_h = oracle.gen_tcp(seed, 0, G, oracle.zipf_cdf(G, 0.8), 0, n)
+        evs.append((ev_h, {k: H.to_device(ev_h[k]) for k in ("pid", "size")}))
+    aggs = [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0), A.Agg(A.AGG_SUM, 1, A.NO_COL, 8, 0)]
+
+    def want(*which):
+        pid = np.concatenate([evs[w][0]["pid"] for w in which])
+        size = np.concatenate([evs[w][0]["size"] for w in which])
+        return oracle.groupby(oracle.pack_cols({"pid": pid}, ("pid",)), [{"kind": "count"}, {"kind": "sum", "val": size}])
+
+    def feed(w, base):
+        ev = evs[w][1]
+        tab.update([ev["pid"], ev["size"]], [0], n, base)
+
+    tab = E.Table([4], aggs, 65536)
+    tab.set_mode(A.GB_CACHED)
+    feed(0, 0)
+    tab.reset()                        # no finalize: the byte map is cleared here
+    feed(1, 0)
+    _check(E, H, tab, [4], *want(1))
+    feed(0, n)                         # same interval, after a finalize
+    _check(E, H, tab, [4], *want(1, 0))
+    for mode in (A.GB_CACHED, A.GB_PART, A.GB_DIRECT, A.GB_CACHED):
+        tab.reset()
+        tab.set_mode(mode)
+        feed(0, 0)
+        _check(E, H, tab, [4], *want(0))
+    tab.destroy()
+
+
 def test_capacity_overflow_is_reported(oracle, E, H, igx, torch):
     A = igx._abi
     G, n = 5000, 200_000
