@@ -20,8 +20,9 @@
 // global atomics): key records are written once per interval and stay L2-resident for
 // the probes, value records only ever receive fire-and-forget atomics.
 // The slot index IS the group id; igx_groupby_finalize lists the occupied slots from a
-// bitmap the claimers set (one bit per slot, so the list costs S/8 bytes, not a walk of
-// every key record).  A reset bumps the epoch instead of rewriting the table: records of an
+// bitmap (one bit per slot, so the list costs S/8 bytes, not a walk of every key record):
+// the partitioned form's claimers set it, the cached form's mark a byte map with plain byte
+// stores that finalize folds into it, the direct form's are read off the tags.  A reset bumps the epoch instead of rewriting the table: records of an
 // older epoch read as empty and the claimer initialises its value record (first =
 // first_ins, aggregates 0) before it publishes `ready`.
 // A new key claims a record with a 64-bit CAS on the tag, writes its key with write-through
