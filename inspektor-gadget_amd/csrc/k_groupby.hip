@@ -1072,7 +1072,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
         // 4. publish the records claimed last iteration (their stores are now complete)
         if (st == PUB) {
             st_agent(reinterpret_cast<uint64_t *>(rec + KOFF + 8), (a.ep << 48) | (x.gidx + 1));
-            a.occb[s] = 1;
+            __builtin_nontemporal_store((uint8_t)1, a.occb + s);
             finish_miss<KW, NA, DBG>(a, c, r, x, s, x.gidx, true);
             st = FREE;
         }
@@ -1233,7 +1233,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
             if (pend_s[j] != SLOT_OVF) {
                 st_agent(reinterpret_cast<uint64_t *>(a.krec + (uint64_t)pend_s[j] * a.krec_len + KOFF + 8),
                          (a.ep << 48) | (pend_g[j] + 1));
-                a.occb[pend_s[j]] = 1;
+                __builtin_nontemporal_store((uint8_t)1, a.occb + pend_s[j]);
                 pend_s[j] = SLOT_OVF;
             }
         }
