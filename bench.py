@@ -89,15 +89,35 @@ def parse(argv=None):
     p.add_argument("--config-steps", type=int, default=20,
                    help="timed steps per other config (C1 at 5 steps: 0.20-0.22 ms, at 50: 0.17 -- the "
                         "closing synchronisation weighs on a 0.2 ms step)")
+    p.add_argument("--batches", type=int, default=0,
+                   help="C2 / C5: pre-generated batches the intervals step through -- consecutive slices of one "
+                        "stream (same key universe and Zipf law, different events), so the keys an interval finds "
+                        "already in the table recur because the stream repeats them, never because a batch is "
+                        "replayed.  0 = one slice per interval (warmup + steps), as many as --input-gb holds; "
+                        "past that the slices rotate")
+    p.add_argument("--input-gb", type=float, default=150.0,
+                   help="HBM for the C2 / C5 input slices (--batches 0)")
     p.add_argument("--no-check", dest="check", action="store_false",
                    help="skip the post-run check of each config's last timed interval against the oracle")
     p.add_argument("--transport", choices=("igx", "torch"), default="torch",
                    help="N>1 exchanges: torch's collectives (RCCL on the nccl group; the default until "
                         "the igx_dist_* send/recv loops have run with two or more GPUs) or the igx_dist_* "
                         "C ABI over RCCL (falls back to torch's if igx_dist_init fails on any rank)")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="N>1 process group: nccl (RCCL over xGMI, one GPU per rank) or gloo -- a rehearsal of the "
+                        "N>1 path whose ranks may share one GPU (tests/test_gpu_bench_dist.py); the product's "
+                        "igx_dist_* transport needs one GPU per rank and is then reported unavailable")
     p.add_argument("--launch-dry-run", action="store_true",
                    help="launcher self-test: each rank prints its RANK/WORLD_SIZE and exits, no GPU")
     return p.parse_args(argv)
+
+
+def n_batches(a, steps, event_bytes, n):
+    """Slices of the stream a config steps through: one per interval when they fit --input-gb."""
+    if a.batches > 0:
+        return a.batches
+    fit = int(a.input_gb * 1e9 // (event_bytes * n))
+    return max(2, min(steps, fit))
 
 
 def free_port():
@@ -295,7 +315,68 @@ def sum_rank_hists(refs):
     return np.sum([r.astype(np.uint64) for r in refs], axis=0).astype(np.uint32)
 
 
-def check_c2(a, ctx, tab, cand, cdf_h, Gn):
+def fingerprint(torch, rows):
+    """Order-independent fingerprint of packed rows on the device: the sum over rows of a 64-bit
+    mix of each row's words (wrapping int64 arithmetic; tests/test_gpu_soak.py's)."""
+    G, rb = rows.shape
+    if G == 0:
+        return 0
+    wb = (rb + 7) // 8 * 8
+    r = torch.zeros((G, wb), dtype=torch.uint8, device=rows.device)
+    r[:, :rb] = rows
+    w = r.view(torch.int64)
+    x = torch.full((G,), 0x243F6A8885A308D3, dtype=torch.int64, device=rows.device)
+    for j in range(w.shape[1]):
+        x = (x ^ w[:, j]) * 0x100000001B3
+        x = x ^ (x >> 29)
+    return int(x.sum().item())
+
+
+IGX_CHECK_TIMEOUT_MS = 30000
+
+
+def transport_check(ctx, what, fn):
+    """N > 1, after a config's timed loop (outside it): the config's exchange run once through
+    torch's collectives and once through the product's own igx_dist_* C ABI (IgxComm: RCCL inside
+    libigx.so, the entry points a cgo caller binds), the results compared byte for byte on every
+    rank; the ranks agree through an all-reduce (MIN).  fn(transport) -> a device u8 tensor.  A
+    C-ABI transport that cannot be opened on some rank is reported (transport_igx_equal None);
+    one that opens and then fails or differs is a mismatch (False: bench.py exits 3)."""
+    torch, dist, D = ctx["torch"], ctx["dist"], ctx["D"]
+    if ctx["world"] == 1:
+        return None
+    rec = {"what": what + ": torch.distributed (nccl = RCCL) vs igx_dist_* (C ABI, RCCL in libigx.so)"}
+    ref = fn(D.TorchComm(dist))
+    if "igx_comm" not in ctx:
+        try:
+            ctx["igx_comm"] = D.IgxComm(dist, timeout_ms=IGX_CHECK_TIMEOUT_MS)
+        except Exception as e:   # noqa: BLE001 -- agreed on below
+            ctx["igx_comm"], ctx["igx_comm_error"] = None, repr(e)[:300]
+        up = torch.tensor([1 if ctx["igx_comm"] is not None else 0], dtype=torch.int32, device=ctx["dev"])
+        dist.all_reduce(up, op=dist.ReduceOp.MIN)
+        if not int(up.item()) and ctx["igx_comm"] is not None:
+            ctx["igx_comm"].close()
+            ctx["igx_comm"] = None
+    ic = ctx["igx_comm"]
+    if ic is None:
+        rec["transport_igx_equal"] = None
+        rec["igx_error"] = ctx.get("igx_comm_error", "igx_dist_init failed on another rank")
+        return rec
+    ok = True
+    try:
+        got = fn(ic)
+        ok = got.shape == ref.shape and bool(torch.equal(got, ref))
+    except Exception as e:   # noqa: BLE001 -- a failed collective (IGX_EIO within the deadline)
+        ok = False
+        rec["igx_error"] = repr(e)[:300]
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=ctx["dev"])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    rec["transport_igx_equal"] = bool(int(flag.item()))
+    rec["bytes"] = int(ref.numel())
+    return rec
+
+
+def check_c2(a, ctx, tab, cand, cdf_h, Gn, base):
     """C2's last timed interval vs or_top_tcp_mt on the same stream: this rank's group count
     and whole-table checksum (key fields, sent, recv, first index of every group), and the
     top-20 (first, sent, recv) -- at N>1 the global top-20 against the oracle's merge of every
@@ -306,8 +387,8 @@ def check_c2(a, ctx, tab, cand, cdf_h, Gn):
     rows = H.host(table_rows(E, torch, tab, tab.fin))
     dev_cs = O.tcp_group_checksum(tcp_fields66(rows), u64_col(rows, 72), u64_col(rows, 80), u64_col(rows, 88))
     del rows
-    h = O.gen_tcp(0xC2, rank, G, cdf_h, rank * N, N)
-    Gref, sent, recv, first, cs = O.top_tcp_mt(h, K, base_idx=rank * N, threads=check_threads(ctx), checksum=True)
+    h = O.gen_tcp(0xC2, rank, G, cdf_h, base, N)
+    Gref, sent, recv, first, cs = O.top_tcp_mt(h, K, base_idx=base, threads=check_threads(ctx), checksum=True)
     del h
     recs = gather_checks(ctx, {"groups": int(Gn), "oracle_groups": int(Gref), "checksum_equal": dev_cs == cs,
                                "sent": sent, "recv": recv, "first": first})
@@ -321,12 +402,13 @@ def check_c2(a, ctx, tab, cand, cdf_h, Gn):
     return {"bit_exact": bool(groups_ok and cs_ok and top_ok), "groups_equal": bool(groups_ok),
             "table_checksum_equal": bool(cs_ok), "topk_equal": bool(top_ok),
             "groups": [r["groups"] for r in recs], "oracle_groups": [r["oracle_groups"] for r in recs],
-            "what": "last timed interval vs oracle or_top_tcp_mt on the same stream: per-rank group count and "
+            "batch_base": base,
+            "what": "last timed interval vs oracle or_top_tcp_mt on its own batch: per-rank group count and "
                     "whole-table checksum (66 key bytes + sent + recv + first of every group), global top-"
                     f"{K} (first, sent, recv)" + (" vs the oracle merge of every rank's top-K" if world > 1 else "")}
 
 
-def check_table(a, ctx, tab, cand, keys_h, oaggs, valid, naggs, sort, K):
+def check_table(a, ctx, tab, cand, keys_h, oaggs, valid, naggs, sort, K, base=0):
     """C4 / C5 (N=1): the last timed interval's table -- group count and a checksum of every
     (key, aggregates, first index) -- and, with `sort`, its top-K against or_groupby_topk_mt."""
     torch, E, H, O = ctx["torch"], ctx["E"], ctx["H"], ctx["O"]
@@ -337,7 +419,7 @@ def check_table(a, ctx, tab, cand, keys_h, oaggs, valid, naggs, sort, K):
                               u64_col(rows, kb + 8 * naggs))
     ng = rows.shape[0]
     del rows
-    Gref, first, aggs, cs = O.groupby_topk_mt(keys_h, oaggs, valid=valid, sort=sort, k=K,
+    Gref, first, aggs, cs = O.groupby_topk_mt(keys_h, oaggs, valid=valid, base_idx=base, sort=sort, k=K,
                                               threads=check_threads(ctx), checksum=True)
     out = {"groups": int(fin["n_groups"]), "oracle_groups": int(Gref), "groups_equal": fin["n_groups"] == Gref == ng,
            "table_checksum_equal": dev_cs == cs}
@@ -376,25 +458,35 @@ def run_c2(a, ctx):
     rank, world = ctx["rank"], ctx["world"]
     N, G, K = a.events, a.keys, a.topk
     cdf_h = E.zipf_cdf(G, a.zipf)
-    base = rank * N                                   # global event index of row 0
-    ev = E.gen_tcp(0xC2, rank, G, H.to_device(cdf_h, ctx["dev"]), base, N)
-    cols = [ev[k] for k in TCP_NAMES] + [ev["size"].view(torch.int32)]   # 10: `int copied`
+    cdf_d = H.to_device(cdf_h, ctx["dev"])
+    # batch b = events [(b * world + rank) * N, ... + N) of one stream: the global event index of
+    # row 0 (the first-index position), so every interval's events are distinct
+    bases = [(b * world + rank) * N for b in range(n_batches(a, a.steps + a.warmup, EV_BYTES, N))]
+    colsets = []
+    for b in bases:
+        ev = E.gen_tcp(0xC2, rank, G, cdf_d, b, N)
+        colsets.append([ev[k] for k in TCP_NAMES] + [ev["size"].view(torch.int32)])   # 10: `int copied`
+    del ev
     aggs = [A.Agg(A.AGG_SUM, 8, 9, 8, 0), A.Agg(A.AGG_SUM, 8, 9, 8, 1)]
     tab = E.Table([16, 16, 8, 4, 16, 2, 2, 2], aggs, capacity=G + G // 4)
     preds = [family_in_pred(A, 7), copied_pred(A, 10, 9)]
     clk = KernelClock(torch)
-    st = {}
+    st = {"i": 0}
 
     def step(record):
+        b = st["i"] % len(bases)
+        st["i"] += 1
+        st["b"] = b
         tab.reset()
         clk.on = record
         with clk:
-            tab.update(cols, list(range(8)), N, base, preds)
+            tab.update(colsets[b], list(range(8)), N, bases[b], preds)
         tab.finalize(sync=False)                      # the group count stays on the device
         # SortStats(["-sent","-recv"]) over the table's groups, first K slots (the device top-K
         # reads the count there: the step has no host round trip)
         cand = tab.gather(tab.sort([(A.TSRC_AGG, 0, True), (A.TSRC_AGG, 1, True)], K))
         if world > 1:
+            st["local"] = cand
             cand = D.merge_topk(cand, 72, 2, [(0, True), (1, True)], K)
         st["cand"] = cand
 
@@ -403,12 +495,18 @@ def run_c2(a, ctx):
     Gn = tab.wait()                                   # the last interval's group count
     alg = N * EV_BYTES + Gn * GROUP_BYTES
     out = {"value": world * N * a.steps / dt, "ms_per_step": dt * 1000.0 / a.steps, "groups_per_gpu": Gn,
+           "batches": len(bases), "claims_per_interval": tab.info()["claims"],
            "roofline": roofline(alg, clk.avg(), "k_groupby<ip_key_t>",
                                 f"{EV_BYTES} B/event x events + {GROUP_BYTES} B/group x groups", "c2",
                                 {"events": N, "keys": G, "zipf": a.zipf})}
     out["roofline"]["hbm_pct_of_peak_whole_step"] = 100.0 * alg / (out["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS
     if a.check:
-        out["check"] = check_c2(a, ctx, tab, st["cand"], cdf_h, Gn)
+        out["check"] = check_c2(a, ctx, tab, st["cand"], cdf_h, Gn, bases[st["b"]])
+        if world > 1:   # every rank takes part; rank 0 records it
+            tr = transport_check(ctx, "C2 all-gather of the per-rank top-K candidates",
+                                 lambda c: D.allgather_rows(st["local"], c).flatten())
+            if out["check"] is not None:
+                out["check"]["transport"] = tr
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = a.cpu_sample
@@ -529,11 +627,19 @@ def run_c3(a, ctx):
         ref = O.hist_log2_mt(hh["dev"], hh["cont"], hh["delta"], devs, C3_NCONT, threads=check_threads(ctx))
         del hh
         refs = gather_checks(ctx, ref)
+        tr = None
+        if world > 1:
+            loc = torch.zeros_like(hist)
+            E.hist_log2(ev["dev"], ev["cont"], delta, devs, C3_NCONT, hist=loc)   # this rank's own histogram
+            tr = transport_check(ctx, "C3 all-reduce of the u32[4096][27] histogram",
+                                 lambda c: D.allreduce_hist(loc.clone(), c).flatten().view(torch.uint8))
         if rank == 0:
             tot = sum_rank_hists(refs)
             ok = bool(np.array_equal(H.host(hist), tot))
             out["check"] = {"bit_exact": ok, "what": "last timed step's whole u32[4096][27] histogram vs the sum "
                                                      f"of {world} rank(s)' oracle histograms"}
+            if tr is not None:
+                out["check"]["transport"] = tr
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 40_000_000
@@ -566,6 +672,8 @@ def run_c4(a, ctx):
     # distinct only, as the reference: graph.c:102-114 (BPF_NOEXIST, first timestamp wins),
     # advisor.go:307-319 (first event per tuple); nothing is counted
     tab = E.Table(widths, [], cap)
+    # an owner receives about 1/N of the global distinct tuples, but C4's tuple universe is not
+    # bounded by one rank's capacity (every rank's slice adds tuples), so its table keeps it
     own = E.Table(widths, [], cap) if world > 1 else None
     clk = KernelClock(torch)
     st = {}
@@ -576,18 +684,20 @@ def run_c4(a, ctx):
         with clk:   # the bracket holds every kernel that reads the 24 B/event: np_mark and the update
             keep = E.np_mark(ev["type"], ev["pkt"], ev["hostip"], ev["raddr"])
             tab.update(cols, [0, 1, 2, 3], n, rank * n, valid=keep)
+        tab.finalize(sync=False)                      # the distinct count stays on the device
         if world > 1:
-            fin = tab.finalize()
-            rows = table_rows(E, torch, tab, fin)
-            mine = D.exchange_rows(rows, fin["key_bytes"])
-            D.merge_partials(mine, widths, [], cap, table=own)
-            st["G"] = own.fin["n_groups"]
-        else:
-            tab.finalize(sync=False)                  # the distinct count is read after the loop
+            # the partial groups, grouped by owner straight from the table (the device count
+            # sizes the passes); the send counts are the step's one host read, then the
+            # exchange's own plan all-gather, then the owner merge, finalized asynchronously
+            rows, cnt = tab.partition(world)
+            counts = cnt.cpu().tolist()
+            mine = D.exchange_partitioned(rows, counts)
+            D.merge_partials(mine, widths, [], cap, table=own, sync=False)
+            st["part"] = (rows, counts)
 
     dt = T.run(step, a.config_steps, 1)
     ms = dt * 1000.0 / a.config_steps
-    ng = st["G"] if world > 1 else tab.wait()
+    ng = own.wait() if world > 1 else tab.wait()
     alg = n * 24 + ng * 20
     out = {"workload": "advise network-policy: np_mark + distinct (src, dir, peer, port) with first index"
                        + (", partial groups all-to-all by key owner + owner merge" if world > 1 else ""),
@@ -608,9 +718,20 @@ def run_c4(a, ctx):
         out["check"]["what"] = ("last timed interval's table vs oracle or_groupby_topk_mt distinct on the same "
                                 "stream: distinct count + checksum of every (tuple, first index)")
         del keys, valid
-    elif a.check and rank == 0:
-        out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
-                                   "tests/test_gpu_dist.py"}
+    elif a.check:
+        scratch = E.Table(widths, [], cap)
+
+        def c4x(c):
+            mine = D.exchange_partitioned(st["part"][0], st["part"][1], c)
+            t = D.merge_partials(mine, widths, [], cap, table=scratch)
+            fp = fingerprint(torch, table_rows(E, torch, t, t.fin))
+            return torch.cat([mine.flatten(), torch.tensor([fp], dtype=torch.int64, device=mine.device).view(torch.uint8)])
+
+        tr = transport_check(ctx, "C4 all-to-all of the partial groups by key owner + the owner merge", c4x)
+        scratch.destroy()
+        if rank == 0:
+            out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
+                                       "tests/test_gpu_dist.py", "transport": tr}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         # the reference's own path: GeneratePolicies builds a localPodKey / networkPeerKey string
@@ -671,58 +792,88 @@ def run_c5(a, ctx):
     G, K = C5_KEYS, C5_TOPK
     names, widths = C5_NAMES, C5_WIDTHS
     cdf_h = E.zipf_cdf(G, C5_ZIPF)
-    ev = E.gen_file(0xC5, 0, G, H.to_device(cdf_h, ctx["dev"]), rank * n, n)   # one global key universe
-    cols = [ev[k] for k in names]
+    cdf_d = H.to_device(cdf_h, ctx["dev"])
+    # one global key universe; batch b is the b-th chunk of one global stream, this rank's slice
+    bases = [(b * world + rank) * n for b in range(n_batches(a, a.config_steps + 1, 25, n))]
+    colsets = []
+    for b in bases:
+        ev = E.gen_file(0xC5, 0, G, cdf_d, b, n)
+        colsets.append([ev[k] for k in names])
+    del ev
     aggs = c5_aggs(A)
     cap = C5_CAP
     tab = E.Table(widths, aggs, cap)
-    own = E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], cap) if world > 1 else None
+    # C5's key universe is global (C5_CAP bounds it), so an owner holds about 1/N of it
+    own_cap = D.owner_capacity(cap, world)
+    own = (E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], own_cap)
+           if world > 1 else None)
     clk = KernelClock(torch)
-    st = {}
+    st = {"i": 0}
 
     def step(record):
+        b = st["i"] % len(bases)
+        st["i"] += 1
+        st["b"] = b
         tab.reset()
         clk.on = record
         with clk:
-            tab.update(cols, [0, 1, 2, 3], n, rank * n)
+            tab.update(colsets[b], [0, 1, 2, 3], n, bases[b])
         t = tab
+        tab.finalize(sync=False)                      # the group count stays on the device
         if world > 1:
-            fin = tab.finalize()
-            st["G"] = fin["n_groups"]
-            rows = table_rows(E, torch, tab, fin)
-            mine = D.exchange_rows(rows, fin["key_bytes"])
-            t = D.merge_partials(mine, widths, [8, 8, 8, 8], cap, table=own)
-        else:
-            tab.finalize(sync=False)                  # the top-K reads the group count on the device
+            # as C4: partition straight from the table, one host read (the send counts), the
+            # exchange, the owner merge finalized asynchronously (its top-K reads its count there)
+            rows, cnt = tab.partition(world)
+            counts = cnt.cpu().tolist()
+            mine = D.exchange_partitioned(rows, counts)
+            t = D.merge_partials(mine, widths, [8, 8, 8, 8], own_cap, table=own, sync=False)
+            st["part"] = (rows, counts)
         cand = t.gather(t.sort([(A.TSRC_AGG, 3, True)], K))       # ["-wbytes"]
         if world > 1:
+            st["local"] = cand
             cand = D.merge_topk(cand, 20, 4, [(3, True)], K)
         st["cand"] = cand
 
     dt = T.run(step, a.config_steps, 1)
     ms = dt * 1000.0 / a.config_steps
-    ng = st["G"] if world > 1 else tab.wait()
+    ng = own.wait() if world > 1 else tab.wait()
     alg = n * 25 + ng * 60
     out = {"workload": "top file: group-by (inode, dev, pid, tid) with reads/rbytes/writes/wbytes, top-20 by "
                        "[-wbytes]" + (", partial groups all-to-all by key owner, owners' top-20 all-gathered"
                                       if world > 1 else ""),
            "events_per_gpu": n, "keys": G, "value": world * n / (ms * 1e-3), "unit": "events/s",
-           "ms_per_step": ms, "groups_on_rank0": ng,
+           "ms_per_step": ms, "groups_on_rank0": ng, "batches": len(bases),
+           "owner_capacity": own_cap if world > 1 else None,
+           "claims_per_interval": tab.info()["claims"] if world == 1 else None,
            "roofline": roofline(alg, clk.avg(), "k_groupby<file_id>",
                                 "25 B/event (inode 8, dev 4, pid 4, tid 4, op 1, count 4) + 60 B/group", "c5",
                                 {"events": n, "keys": G})}
     if a.check and world == 1:
         O = ctx["O"]
-        h = O.gen_file(0xC5, 0, G, cdf_h, 0, n)
+        base = bases[st["b"]]
+        h = O.gen_file(0xC5, 0, G, cdf_h, base, n)
         keys = O.pad_keys(h, ("inode", "dev", "pid", "tid"))
-        out["check"] = check_table(a, ctx, tab, st["cand"], keys, c5_oracle_aggs(h), None, 4, [(3, True)], K)
-        out["check"]["what"] = ("last timed interval's table vs oracle or_groupby_topk_mt on the same stream: "
+        out["check"] = check_table(a, ctx, tab, st["cand"], keys, c5_oracle_aggs(h), None, 4, [(3, True)], K, base)
+        out["check"]["batch_base"] = base
+        out["check"]["what"] = ("last timed interval's table vs oracle or_groupby_topk_mt on its own batch: "
                                 "group count, checksum of every (key, reads, rbytes, writes, wbytes, first), "
                                 "top-20 by [-wbytes] (first + 4 aggregates)")
         del h, keys
-    elif a.check and rank == 0:
-        out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
-                                   "tests/test_gpu_dist.py"}
+    elif a.check:
+        scratch = E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], own_cap)
+
+        def c5x(c):
+            mine = D.exchange_partitioned(st["part"][0], st["part"][1], c)
+            t = D.merge_partials(mine, widths, [8, 8, 8, 8], own_cap, table=scratch)
+            allc = D.allgather_rows(t.gather(t.sort([(A.TSRC_AGG, 3, True)], K)), c)
+            return torch.cat([mine.flatten(), allc.flatten()])
+
+        tr = transport_check(ctx, "C5 all-to-all of the partial groups by key owner + owner merge + all-gather "
+                                  "of the owners' top-20", c5x)
+        scratch.destroy()
+        if rank == 0:
+            out["check"] = {"skipped": "N>1: the owners' tables span every rank's slice; checked at N=1 and by "
+                                       "tests/test_gpu_dist.py", "transport": tr}
     if rank == 0 and world == 1 and a.cpu_sample:
         O = ctx["O"]
         S = 10_000_000
@@ -766,11 +917,15 @@ def main():
     import torch
     import torch.distributed as dist
 
+    local = local % max(1, torch.cuda.device_count())   # a gloo rehearsal may run more ranks than GPUs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     transport = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     igx = importlib.import_module("inspektor-gadget_amd")
     if world > 1:
@@ -804,6 +959,8 @@ def main():
                             "pid,comm,lport,dport,family) sum sent/recv, stable top-20 by [-sent,-recv]",
                 "events_per_gpu": a.events, "keys_per_gpu": a.keys, "zipf_s": a.zipf, "topk": a.topk,
                 "groups_per_gpu": c2["groups_per_gpu"],
+                "batches": c2["batches"],
+                "claims_per_interval": c2["claims_per_interval"],
                 "parallelism": (f"ingest-partitioned x{world}, all-gather top-K merge over "
                                 + ("igx_dist_* (RCCL, C ABI)" if transport == "igx" else
                                    "torch.distributed (nccl = RCCL)")) if world > 1 else "single GPU",
@@ -818,10 +975,17 @@ def main():
             line["check"]["configs"] = {k: v["check"].get("bit_exact", "skipped")
                                         for k, v in configs.items() if "check" in v}
             failed = [k for k, v in [("c2", c2)] + list(configs.items())
-                      if v.get("check", {}).get("bit_exact") is False]
+                      if v.get("check", {}).get("bit_exact") is False
+                      or (v.get("check", {}).get("transport") or {}).get("transport_igx_equal") is False]
+            if world > 1:
+                line["check"]["transport_igx_equal"] = {
+                    k: (v.get("check", {}).get("transport") or {}).get("transport_igx_equal")
+                    for k, v in [("c2", c2)] + list(configs.items())}
             line["check"]["all_bit_exact"] = not failed
         print(json.dumps(line), flush=True)
     if world > 1:
+        if ctx.get("igx_comm") is not None:
+            ctx["igx_comm"].close()
         igx.dist.shutdown()
         dist.destroy_process_group()
     if failed:

@@ -337,7 +337,9 @@ typedef struct {
                             that missed the LDS cache on > 39 % of their rows, until one falls below 37 %) */
     uint64_t rows;       /* rows fed to the interval so far */
     uint32_t miss_permille;  /* LDS misses per 1000 rows of the last measured cached interval */
-    uint32_t pad;
+    uint32_t persist;    /* 1: keys are kept across intervals (a generation; igx_groupby_reset) */
+    uint64_t claims;     /* the last collected finalize: keys its interval inserted (the others were kept) */
+    uint64_t gen_keys;   /* ... keys the table's generation held after it (UINT64_MAX: it ended) */
 } igx_groupby_info_t;
 int igx_groupby_info(igx_table *t, igx_groupby_info_t *out);
 /* igx_groupby_finalize without its host synchronisation: the occupied-slot list is built on
@@ -365,7 +367,14 @@ int igx_groupby_wait(igx_table *t, uint64_t *n_groups);
  * nextStats builds (pkg/gadgets/top/tcp/tracer/tracer.go:186-219).  Call after
  * igx_groupby_finalize.  Asynchronous. */
 int igx_groupby_gather(igx_table *t, const uint32_t *idx, uint64_t k, uint8_t *out_rows);
-int igx_groupby_reset(igx_table *t); /* per-interval reset (nextStats' Delete loop) */
+/* Per-interval reset (nextStats' Delete loop, tracer.go:154-171): the next interval's groups,
+ * sums and first indices are its own.  Keys themselves are kept across intervals while the
+ * table runs its cached form: a recurring key is found instead of inserted again, and only the
+ * last interval's groups' value records are cleared.  The kept keys end (the next interval
+ * starts an empty table) when they plus `capacity` new ones would fill more than 4/5 of the
+ * slots, after a failed interval, when an interval runs the direct or partitioned form, or
+ * with IGX_GB_PERSIST=0.  Asynchronous. */
+int igx_groupby_reset(igx_table *t);
 /* How updates run (results are identical in every mode):
  *   IGX_GB_CACHED  one workgroup per CU with an LDS cache of hot keys (Zipf-like streams:
  *                  most rows never leave the CU);
@@ -387,10 +396,14 @@ int igx_groupby_set_mode(igx_table *t, uint32_t mode);
 int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uint32_t k,
                      uint32_t *out_slots);
 int igx_groupby_destroy(igx_table *t);
-/* Diagnostics only (IGX_GB_DEBUG env): out8[0..1] LDS-cache hits / misses (bit 3); out8[4..7]
- * sleep counts of loaders on a full miss ring, probers on an empty one, probers on a full
- * update ring, the idle server (bit 16).  Counters since the last call. */
-int igx_groupby_debug_counts(igx_table *t, uint64_t *out8);
+/* Diagnostics only (IGX_GB_DEBUG env), 32 words: out[0..1] LDS-cache hits / misses (bit 3);
+ * out[4..7] sleep counts of loaders on a full miss ring, probers on an empty one, probers on a
+ * full update ring, the idle server (bit 16); bit 18, the memory-side atomics: out[8..11] the
+ * server wave's updates, of them minima, distinct (value record, opcode) pairs per instruction,
+ * distinct (128-B line, opcode) pairs; [12] instructions whose first record continues the
+ * previous one's last; [16..19] the same four for the final LDS flush's aggregate updates, [20]
+ * its minima.  Counters since the last call. */
+int igx_groupby_debug_counts(igx_table *t, uint64_t *out32);
 
 /* ---- advise network-policy -------------------------------------------------------------- */
 /* keep[i] = 1 iff the advisor would consider event i (advisor.go:279-292): type == normal
@@ -446,6 +459,15 @@ int igx_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t addr_stride, const u
  * mod nparts (1..64).  part_counts (device u64[nparts]) receives the rows per part.  Async. */
 int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nrows, uint32_t row_bytes,
                        uint32_t key_bytes, uint32_t nparts, uint8_t *out, uint64_t *part_counts);
+/* The same partition straight from a finalized table (igx_groupby_finalize or _async): its
+ * groups as igx_groupby_gather rows (key words | aggregates wrapped to out_widths[x] bytes
+ * (nullable: 8) | first index) grouped by owner part, stable in slot order within a part.  The
+ * group count is read on the device (view->d_n_groups), so an asynchronously finalized table
+ * is partitioned without a host round trip; out holds cap_rows rows (>= the table's capacity).
+ * The sender side of the owner exchange (C4 / C5 at N > 1; replaces the reference's per-node
+ * fan-out + client merge, grpc-runtime.go:221-237 -> snapshotcombiner.go:79-106).  Async. */
+int igx_partition_groups(igx_ctx *ctx, const igx_table_view *view, const uint32_t *out_widths,
+                         uint32_t nparts, uint8_t *out, uint64_t cap_rows, uint64_t *part_counts);
 /* ---- multi-GPU merges over RCCL ----------------------------------------
  * One process per GPU.  Replaces the reference's node fan-out + client concatenation
  * (pkg/runtime/grpc/grpc-runtime.go:221-237 -> pkg/snapshotcombiner/snapshotcombiner.go:79-106)

@@ -55,7 +55,8 @@ class SortKey(C.Structure):
 class GroupbyInfo(C.Structure):
     _fields_ = [("form", C.c_uint32), ("region", C.c_uint32), ("part_left", C.c_uint32),
                 ("exact_left", C.c_uint32), ("sm_probers", C.c_uint32), ("loaders", C.c_uint32),
-                ("rows", C.c_uint64), ("miss_permille", C.c_uint32), ("pad", C.c_uint32)]
+                ("rows", C.c_uint64), ("miss_permille", C.c_uint32), ("persist", C.c_uint32),
+                ("claims", C.c_uint64), ("gen_keys", C.c_uint64)]
 
 
 class Agg(C.Structure):
@@ -157,6 +158,7 @@ SIGNATURES = [
                            _VP]),
     ("igx_log2_slots", _I, [_VP, _VP, _U64, _U64, _U32, _VP, _VP]),
     ("igx_partition_rows", _I, [_VP, _VP, _U64, _U32, _U32, _U32, _VP, _VP]),
+    ("igx_partition_groups", _I, [_VP, _VP, _VP, _U32, _VP, _U64, _VP]),
     ("igx_dist_get_unique_id", _I, [_VP]),
     ("igx_dist_init", _I, [_VP, _VP, _I, _I, C.POINTER(_VP)]),
     ("igx_dist_destroy", _I, [_VP]),

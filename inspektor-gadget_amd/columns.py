@@ -255,7 +255,8 @@ class EventBatch:
             sel = idx
         else:
             from . import engine
-            sel = engine.take([self.sel], idx, self.n)[0]
+            n = self.n    # read first: reading n trims a pending (device-count) selection
+            sel = engine.take([self.sel], idx, n)[0]
         return EventBatch(self.cols, self._base, self._base_valid, sel=sel)
 
     def materialize(self):

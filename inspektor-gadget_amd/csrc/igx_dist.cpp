@@ -310,8 +310,9 @@ extern "C" int igx_dist_destroy(igx_dist *d) {
         drained = dist_sync(d, "dist_destroy") == IGX_OK;   // aborts the communicator on failure
     } else {
         const double t0 = now_ms();
+        const int bound = d->broken ? std::min(d->timeout_ms, 2000) : d->timeout_ms;   // broken: deadline spent
         hipError_t e;
-        while ((e = hipStreamQuery(d->ctx->stream)) == hipErrorNotReady && now_ms() - t0 < d->timeout_ms)
+        while ((e = hipStreamQuery(d->ctx->stream)) == hipErrorNotReady && now_ms() - t0 < bound)
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         drained = e == hipSuccess;
     }
@@ -321,7 +322,12 @@ extern "C" int igx_dist_destroy(igx_dist *d) {
             d->comm = nullptr;
         }
     }
-    if (!dist_reap(d, d->timeout_ms)) drained = false;   // an abort still blocked: keep the buffers
+    // a broken communicator already spent its deadline in the call that failed (and, above, in
+    // the drain): its aborter gets a short bound here, so destroy waits at most one deadline plus
+    // that bound.  An aborter still blocked is detached by dist_reap and stays
+    // inside ncclCommAbort; its buffers are kept (a process exiting meanwhile ends it with the
+    // process: it touches nothing this library frees).
+    if (!dist_reap(d, d->broken ? std::min(d->timeout_ms, 2000) : d->timeout_ms)) drained = false;
     if (drained) {
         (void)hipFree(d->d_meta);
         (void)hipHostFree(d->h_meta);

@@ -11,6 +11,8 @@
 //            sums its tile's predecessors itself instead)
 //   compact  re-reads only the bitmask (n/8 bytes) and writes the u32 row ids
 // Algorithmic bytes per row = sum of predicate column widths + 4 per survivor.
+#include <cstdlib>
+
 #include "k_common.h"
 
 namespace {
@@ -273,7 +275,9 @@ int launch_filter_chunks(igx_ctx *ctx, const DevPreds *dps, uint32_t nchunks, ui
             hipLaunchKernelGGL(k_filter_mark, dim3(ntiles), dim3(TB), 0, ctx->stream, dps[c], valid, nrows,
                                mask, cnt, any, c > 0 ? 1u : 0u, nil_bit);
     }
-    if (ntiles <= SF_MAX_TILES) {
+    uint64_t sf_max = SF_MAX_TILES;
+    if (const char *e = std::getenv("IGX_FILTER_SF_MAX")) sf_max = std::strtoull(e, nullptr, 0);   // A/B knob
+    if (ntiles <= sf_max) {
         hipLaunchKernelGGL(k_filter_compact_sf, dim3(ntiles), dim3(TB), 0, ctx->stream, mask, cnt, ntiles, out_idx,
                            out_n);
     } else {

@@ -10,10 +10,13 @@
 // HBM table: S = 2^k slots (S >= 2 x capacity), open addressing with linear probing.
 // Each slot has a key record (KR = 32..256 B, one cache line for every built-in layout):
 //     [0, KOFF)            key words (KW x u32, packed; each key column padded to 4 B)
-//     KOFF                 u64 tag   (hash bits 16..63 | epoch; another epoch = empty)
-//     KOFF + 8             u64 ready (epoch << 48 | first_ins + 1; another epoch = key not
-//                          yet published.  first_ins is the claiming event's index, an
-//                          upper bound of the group's first)
+//     KOFF                 u64 tag   (hash bits 16..63 | generation; another generation = empty)
+//     KOFF + 8             u64 ready (epoch << 48 | first_ins + 1.  An epoch before the
+//                          generation's = key not yet published; the interval's own epoch =
+//                          first_ins is this interval's: an upper bound of the group's first,
+//                          whose value record holds first <= first_ins (or will, once the
+//                          interval's atomics land); an earlier epoch of the generation = a
+//                          key kept from an earlier interval, not yet seen in this one)
 // and a value record (VR = 8 x 2^m B):  u64 first (first-occurrence event index), then
 // u64 aggregate a at 8 + 8a.  The two are kept apart because 64-bit atomics execute at
 // the memory side and drop their line from L2 (MI355X_MICROARCH.md, store flavours and
@@ -25,6 +28,17 @@
 // stores that finalize folds into it, the direct form's are read off the tags.  A reset bumps the epoch instead of rewriting the table: records of an
 // older epoch read as empty and the claimer initialises its value record (first =
 // first_ins, aggregates 0) before it publishes `ready`.
+// Keys outlive their interval (a *generation* spans intervals): the reference drains its BPF
+// map every interval (tcp/tracer/tracer.go:154-171) and re-inserts every recurring key, here a
+// reset that continues the generation only returns the previous interval's groups' value
+// records to (first = UINT64_MAX, sums 0), from finalize's slot list.  The first miss of a kept
+// key in an interval finds it (no CAS, no key or value-record stores): it re-stamps `ready`
+// with the interval's epoch and first_ins = its index + 1 (so its own first-index minimum is
+// pushed like any earlier event's) and marks the occupancy byte.  So the interval's output is
+// still exactly its own groups, sums and first indices.  A generation ends (the next interval
+// starts an empty one: tag bits = that interval's epoch) when the keys it holds plus a full
+// interval's capacity would pass 4/5 of the slots, after a failed interval, when the
+// interval runs the direct or partitioned form, or at the epoch counter's wrap.
 // A new key claims a record with a 64-bit CAS on the tag, writes its key with write-through
 // (sc1) stores and publishes `ready` with an sc1 store after `s_waitcnt vmcnt(0)`; readers
 // load the key record with 16-byte sc1 buffer loads (one round trip) and compare the key
@@ -84,6 +98,16 @@ constexpr uint64_t EP_MAX = 0xFFFF;              // epoch bits in a tag / in `re
 constexpr uint64_t READY_IDX = (1ull << 48) - 1;  // `ready` = epoch << 48 | (first_ins + 1)
 
 __device__ __forceinline__ bool ready_ok(uint64_t ready, uint64_t ep) { return (ready >> 48) == ep; }
+// published in the generation that started at epoch gep (the interval's epoch is ep >= gep;
+// epochs only grow within a generation: the counter's wrap clears the table)
+__device__ __forceinline__ bool ready_pub(uint64_t ready, uint32_t gep, uint64_t ep) {
+    const uint64_t r = ready >> 48;
+    return r >= gep && r <= ep;
+}
+// the device generation block behind the error block (u64 words of igx_table::err):
+// [3] the generation's first epoch (tag bits), [4] keys claimed in the generation before this
+// interval (~0: end it), [5] keys claimed in this interval
+constexpr int GEN_WORD = 3;
 
 __host__ __device__ constexpr uint32_t koff_of(int kw) { return (uint32_t)((4 * kw + 7) & ~7); }
 __host__ __device__ constexpr uint32_t pow2_at_least(uint32_t b) {
@@ -154,7 +178,10 @@ struct GbArgs {
                             // 1 with a plain byte store (no atomic: one claimer per slot), finalize
                             // folds it into the bitmap (k_slots_count)
     uint64_t ep;            // the interval's epoch (1..EP_MAX): tags and `ready` of older
-                            // epochs read as empty
+                            // epochs read as empty (the direct and partitioned forms, which
+                            // always start a generation: their generation is ep)
+    uint64_t *gen;          // the device generation block (GEN_WORD): the cached form reads its
+                            // generation there and counts its claims into it
     uint64_t rmask;         // probe region slots - 1 (probing wraps inside a region)
     uint32_t sshift;        // home slot = h >> sshift (the hash's top bits)
     uint32_t max_probe;
@@ -163,6 +190,12 @@ struct GbArgs {
     // hits/misses, bit8 no HBM probe (a hash-derived slot), bit9 no LDS accumulate on hits
     uint32_t dbg;
     unsigned long long *dbg_cnt;
+    // sample-seeded LDS cache (cached form, kept keys): nseeds records of seed_words u32 each
+    // (key words padded to quads | HBM slot | pad | hash) that every workgroup adopts into its
+    // cache before the stream starts, when they belong to the current generation (*seed_gep)
+    const uint32_t *seeds;
+    const uint64_t *seed_gep;
+    uint32_t nseeds;
 };
 
 // Key hash: NH (the UMAC inner hash) over the key's word pairs -- one 32x32->64 multiply
@@ -847,11 +880,47 @@ __device__ __forceinline__ void ring_push(const GbArgs &a, const Ring &r, uint32
     }
 }
 
+// Diagnostics (IGX_GB_DEBUG bit 18, the debug kernels only): what one wave-wide atomic
+// instruction becomes at the memory side, counted into dbg_cnt[base ..]: +0 lanes, +1 of them
+// minima, +2 distinct (value record, opcode) pairs -- the L2 sends a record's same-opcode lanes
+// of one instruction as one request --, +3 distinct (128-B line, opcode) pairs,
+// +4 instructions whose first record continues the previous instruction's last (a miss's
+// updates split over two instructions).  Kept per wave in registers, added at the end.
+__device__ __forceinline__ void atomics_account(const GbArgs &a, bool live, uint32_t slot, bool is_min, uint32_t lane,
+                                                uint32_t base) {
+    uint64_t todo = __ballot(live);
+    if (!todo) return;
+    const uint64_t nmin = (uint64_t)__popcll(__ballot(live && is_min));
+    uint64_t recs = 0, lines = 0;
+    const uint32_t per_line = max(1u, 128u / (a.vrec_words * 8));
+    while (todo) {
+        const uint32_t l = (uint32_t)__ffsll((long long)todo) - 1;
+        const uint32_t s0 = __shfl(slot, (int)l), k0 = __shfl((uint32_t)is_min, (int)l);
+        todo &= ~__ballot(live && slot == s0 && (uint32_t)is_min == k0);
+        ++recs;
+    }
+    todo = __ballot(live);
+    while (todo) {
+        const uint32_t l = (uint32_t)__ffsll((long long)todo) - 1;
+        const uint32_t s0 = __shfl(slot, (int)l) / per_line, k0 = __shfl((uint32_t)is_min, (int)l);
+        todo &= ~__ballot(live && slot / per_line == s0 && (uint32_t)is_min == k0);
+        ++lines;
+    }
+    const uint64_t nlive = (uint64_t)__popcll(__ballot(live));
+    if (lane == 0) {
+        atomicAdd(a.dbg_cnt + base, (unsigned long long)nlive);
+        atomicAdd(a.dbg_cnt + base + 1, (unsigned long long)nmin);
+        atomicAdd(a.dbg_cnt + base + 2, (unsigned long long)recs);
+        atomicAdd(a.dbg_cnt + base + 3, (unsigned long long)lines);
+    }
+}
+
 // the server wave: issue ring entries in order until every producer is done and the ring
 // is empty
 template <bool DBG>
 __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint32_t lane) {
     uint32_t head = 0;
+    [[maybe_unused]] uint32_t prev_last = 0xFFFFFFFFu;   // diagnostics: the last record of the previous instruction
     for (;;) {
         const uint32_t t = __hip_atomic_load(&r.ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (t == head) {
@@ -863,6 +932,7 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
             continue;                      // they bound their own waits)
         }
         const uint32_t n = min(t - head, 64u);
+        uint32_t slot = 0xFFFFFFFFu, what = 0;
         if (lane < n) {
             const uint32_t p = head + lane;
             uint64_t w;
@@ -874,7 +944,8 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
                 if (++spins > SPIN_LIMIT) { atomicOr(a.err, 16u); break; }
             }
             const uint64_t val = r.hi[p % ARING];
-            const uint32_t slot = (uint32_t)w, what = (uint32_t)(w >> 32) & 15u;
+            slot = (uint32_t)w;
+            what = (uint32_t)(w >> 32) & 15u;
             if (DBG && (a.dbg & 131072u)) {   // diagnostics: plain stores instead of the atomics
                 if (what == WHAT_MIN) *rec_first(a, slot) = val;
                 else *rec_agg(a, slot, (int)what) = val;
@@ -882,6 +953,12 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
                 if (what == WHAT_MIN) gmin(rec_first(a, slot), val);
                 else gadd(rec_agg(a, slot, (int)what), val);
             }
+        }
+        if (DBG && (a.dbg & 262144u)) {
+            atomics_account(a, lane < n, slot, what == WHAT_MIN, lane, 8);
+            const uint32_t first_slot = __shfl(slot, 0), last_slot = __shfl(slot, (int)(n - 1));
+            if (lane == 0 && first_slot == prev_last) atomicAdd(a.dbg_cnt + 12, 1ull);
+            prev_last = last_slot;
         }
         head += n;
         if (lane == 0) __hip_atomic_store(&r.ctl[1], head, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -990,9 +1067,26 @@ __device__ __forceinline__ void finish_miss(const GbArgs &a, const LdsCache<KW> 
     else ring_push<NA>(a, r, gs, x.v, x.gidx, first_ins);
 }
 
+// A kept key's first miss of the interval (its `ready` carries an earlier epoch of the
+// generation): `ready` takes the interval's epoch and first_ins = gidx + 1 -- an upper bound the
+// value record will meet, because this event's own minimum is pushed (gidx < first_ins) -- and
+// the slot is marked occupied.  Racing re-stamps of one key each push their own minimum, so
+// whichever `ready` lands, every later reader's first_ins is met.  Returns the first_ins to use.
+template <int KW>
+__device__ __forceinline__ uint64_t restamp(const GbArgs &a, uint64_t s, uint64_t gidx) {
+    if (gidx + 1 >= READY_IDX) {   // an index column value that `ready` cannot carry
+        atomicOr(a.err, 8u);
+        return READY_IDX;          // still correct: every event pushes its minimum
+    }
+    st_agent(reinterpret_cast<uint64_t *>(a.krec + s * a.krec_len + koff_of(KW) + 8), (a.ep << 48) | (gidx + 2));
+    __builtin_nontemporal_store((uint8_t)1, a.occb + s);
+    return gidx + 1;
+}
+
 template <int KW, int NA, bool DBG>
 __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
-                                          const MissRing<KW, NA> &m, uint32_t lane) {
+                                          const MissRing<KW, NA> &m, uint32_t lane, uint32_t gep,
+                                          uint32_t *nclaim) {
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
     constexpr uint32_t FREE = 0, PROBE = 1, CASQ = 2, PUB = 3;
@@ -1058,7 +1152,7 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
         }
         idle = 0;
         // 2. issue this round trip's loads and claims
-        const uint64_t tag = (x.h & ~EP_MAX) | a.ep;
+        const uint64_t tag = (x.h & ~EP_MAX) | gep;
         uint8_t *rec = a.krec + (uint64_t)s * a.krec_len;
         uint32_t d[NQ * 4];
         uint64_t cas_old = 0;
@@ -1098,23 +1192,28 @@ __device__ __forceinline__ void prober_sm(const GbArgs &a, const LdsCache<KW> &c
                 if (++probes >= a.max_probe) { atomicOr(a.err, 4u); st = FREE; }
             }
         }
+        {   // this round's claims (every earlier PUB lane published in step 4)
+            const uint64_t pub = __ballot(st == PUB);
+            if (pub && lane == 0) atomicAdd(nclaim, (uint32_t)__popcll(pub));
+        }
         // 6. probe results (lanes that lost a claim in step 5 read their record next round)
         if (probed && st == PROBE) {
             const uint64_t t = (uint64_t)d[KOFF / 4] | ((uint64_t)d[KOFF / 4 + 1] << 32);
             const uint64_t ready = (uint64_t)d[KOFF / 4 + 2] | ((uint64_t)d[KOFF / 4 + 3] << 32);
-            if ((t & EP_MAX) != a.ep) {
-                expect = t;          // empty in this interval: claim it next round trip
+            if ((t & EP_MAX) != gep) {
+                expect = t;          // empty in this generation: claim it next round trip
                 st = CASQ;
                 if (++tries > (1u << 18)) { atomicOr(a.err, 2u); st = FREE; }
             } else if (t == tag) {
-                if (!ready_ok(ready, a.ep)) {
+                if (!ready_pub(ready, gep, a.ep)) {
                     if (++tries > (1u << 18)) { atomicOr(a.err, 2u); st = FREE; }   // the claimer is still writing
                 } else {
                     bool eq = true;
 #pragma unroll
                     for (int w = 0; w < KW; ++w) eq = eq && (d[w] == x.k[w]);
                     if (eq) {
-                        finish_miss<KW, NA, DBG>(a, c, r, x, s, (ready & READY_IDX) - 1);
+                        const uint64_t fi = (ready >> 48) == a.ep ? (ready & READY_IDX) - 1 : restamp<KW>(a, s, x.gidx);
+                        finish_miss<KW, NA, DBG>(a, c, r, x, s, fi);
                         st = FREE;
                     } else if (!reread) {
                         reread = 1;  // the key quads may predate `ready`: read once more
@@ -1217,7 +1316,8 @@ __device__ __forceinline__ void claim_store_coop(const GbArgs &a, bool claim, ui
 // HBM-update ring.
 template <int KW, int NA, bool DBG, int PB>
 __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, const Ring &r,
-                                       const MissRing<KW, NA> &m, uint32_t lane) {
+                                       const MissRing<KW, NA> &m, uint32_t lane, uint32_t gep,
+                                       uint32_t *nclaim) {
     constexpr uint32_t KOFF = koff_of(KW);
     constexpr int NQ = probe_quads<KW>();
     const __amdgpu_buffer_rsrc_t rs = rec_rsrc(a);
@@ -1305,14 +1405,14 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
             publish();   // waits for this round's probe loads, which it needs anyway
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
-                const uint64_t tag = (x[j].h & ~EP_MAX) | a.ep;
+                const uint64_t tag = (x[j].h & ~EP_MAX) | gep;
                 bool won = false;
                 if (act[j]) {
                     uint8_t *rec = a.krec + s[j] * a.krec_len;
                     uint64_t t = (uint64_t)d[j][KOFF / 4] | ((uint64_t)d[j][KOFF / 4 + 1] << 32);
                     uint64_t ready = (uint64_t)d[j][KOFF / 4 + 2] | ((uint64_t)d[j][KOFF / 4 + 3] << 32);
                     bool next = false;
-                    if ((t & EP_MAX) != a.ep) {   // empty in this interval: claim it
+                    if ((t & EP_MAX) != gep) {   // empty in this generation: claim it
                         if (x[j].gidx >= READY_IDX) {   // an index column value that `ready` cannot carry
                             atomicOr(a.err, 8u);
                             act[j] = false;
@@ -1331,7 +1431,7 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                     }
                     if (act[j]) {
                         if (t == tag) {
-                            if (!ready_ok(ready, a.ep)) {
+                            if (!ready_pub(ready, gep, a.ep)) {
                                 if (++tries[j] > (1u << 22)) { atomicOr(a.err, 2u); act[j] = false; }   // read again
                             } else {
                                 bool eq = true;
@@ -1339,7 +1439,8 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                                 for (int w = 0; w < KW; ++w) eq = eq && (d[j][w] == x[j].k[w]);
                                 if (eq) {
                                     gs[j] = (uint32_t)s[j];
-                                    first_ins[j] = (ready & READY_IDX) - 1;
+                                    first_ins[j] = (ready >> 48) == a.ep ? (ready & READY_IDX) - 1
+                                                                         : restamp<KW>(a, s[j], x[j].gidx);
                                     act[j] = false;
                                 } else if (!reread[j]) {
                                     // the quads of one snapshot are separate loads: `ready` may have
@@ -1359,7 +1460,8 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
                         if (++probes[j] >= a.max_probe) { atomicOr(a.err, 4u); act[j] = false; }
                     }
                 }
-                if (__ballot(won)) {
+                if (const uint64_t wm = __ballot(won)) {
+                    if (lane == 0) atomicAdd(nclaim, (uint32_t)__popcll(wm));
                     claim_store_coop<KW, NA, false>(a, won, (uint32_t)s[j], x[j].k, tag, x[j].gidx, x[j].v);
                     if (won) {   // published by the next publish() (next round or next batch)
                         pend_s[j] = (uint32_t)s[j];
@@ -1421,12 +1523,31 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     for (uint32_t e = threadIdx.x; e < GHOST; e += GTB) c.ghost[e] = 0;
     if (threadIdx.x < 8) ring_ctl[threadIdx.x] = 0;
     __syncthreads();
+    if (a.nseeds && *a.seed_gep == *a.gen) {
+        // the keys a row sample counted most often, adopted by every workgroup up front (their
+        // slots are the generation's: the seeds were looked up in it)
+        constexpr uint32_t SW = LdsCache<KW>::KP + 4;
+        for (uint32_t i = threadIdx.x; i < a.nseeds; i += GTB) {
+            const uint32_t *sr = a.seeds + (uint64_t)i * SW;
+            const uint32_t slot = sr[LdsCache<KW>::KP];
+            if (slot == SLOT_OVF) continue;
+            uint32_t k[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) k[w] = sr[w];
+            const uint64_t h = (uint64_t)sr[LdsCache<KW>::KP + 2] | ((uint64_t)sr[LdsCache<KW>::KP + 3] << 32);
+            (void)lds_adopt<KW>(c, k, h, slot);
+        }
+        __syncthreads();
+    }
 
     if (wave == NWAVES - 1 && !a.direct) {
         ring_serve<DBG>(a, r, lane);
     } else if (wave >= a.nl) {
-        if (a.sm) prober_sm<KW, NA, DBG>(a, c, r, m, lane);
-        else prober<KW, NA, DBG, 1>(a, c, r, m, lane);
+        // the generation this interval belongs to (the reset kernel decided it on the device)
+        const uint32_t gep = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(uint32_t)__hip_atomic_load(a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (a.sm) prober_sm<KW, NA, DBG>(a, c, r, m, lane, gep, &ring_ctl[3]);
+        else prober<KW, NA, DBG, 1>(a, c, r, m, lane, gep, &ring_ctl[3]);
         if (lane == 0) atomicAdd(&r.ctl[2], 1u);
     } else {
         const uint32_t PTB = a.nl * 64;   // rows per workgroup step
@@ -1470,20 +1591,30 @@ __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     // lanes of one instruction into its value record -- one memory-side request per record (the
     // update ring's shape) instead of one per aggregate from a lane that owns the entry
     const uint32_t na = a.naggs;
-    for (uint32_t q = threadIdx.x; q < E * na; q += GTB) {
+    for (uint32_t q0 = threadIdx.x & ~63u; q0 < E * na; q0 += GTB) {   // whole waves (the diagnostics' ballots)
+        const uint32_t q = q0 + lane;
         const uint32_t e = q / na, x = q - e * na;
-        const uint32_t gs = c.st[e];
+        const uint32_t gs = q < E * na ? c.st[e] : ST_EMPTY;
         const uint64_t s = gs < ST_BUSY ? c.agg[x * E + e] : 0ull;
         if (s) gadd(rec_agg(a, gs, (int)x), (unsigned long long)s);
+        if (DBG && (a.dbg & 262144u)) atomics_account(a, s != 0, gs, false, lane, 16);
     }
     for (uint32_t e = threadIdx.x; e < E; e += GTB) {
         const uint32_t gs = c.st[e];
         if (gs >= ST_BUSY) continue;
         const uint64_t f = c.first[e];
-        const uint64_t fi = (ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
-                                                                         koff_of(KW) + 8)) & READY_IDX) - 1;
+        const uint64_t rd = ld_agent(reinterpret_cast<const uint64_t *>(a.krec + (uint64_t)gs * a.krec_len +
+                                                                        koff_of(KW) + 8));
+        // a `ready` not (yet visibly) of this interval bounds nothing: push the minimum
+        const uint64_t fi = (rd >> 48) == a.ep ? (rd & READY_IDX) - 1 : ~0ull;
         if (f < fi) gmin(rec_first(a, gs), (unsigned long long)f);
+        // a seeded key may have had only LDS hits (never probed, so nothing marked it): every
+        // entry with events marks its group occupied (the adopted ones again, harmlessly)
+        if (a.nseeds && f != ~0ull) __builtin_nontemporal_store((uint8_t)1, a.occb + gs);
+        if (DBG && (a.dbg & 262144u) && f < fi) atomicAdd(a.dbg_cnt + 20, 1ull);   // flush minima
     }
+    if (threadIdx.x == 0 && ring_ctl[3])   // the workgroup's claims: the generation's key count
+        atomicAdd(reinterpret_cast<unsigned long long *>(a.gen + 2), (unsigned long long)ring_ctl[3]);
 }
 
 // ---- AUTO's re-probe: the cached form's LDS miss share, estimated ---------------------------
@@ -1534,6 +1665,56 @@ __global__ __launch_bounds__(GTB) void k_gb_estimate(GbArgs a, uint64_t nsample)
     }
     for (int o = 32; o > 0; o >>= 1) nmiss += __shfl_xor(nmiss, o);
     if (lane == 0 && nmiss) atomicAdd(reinterpret_cast<unsigned long long *>(a.err + 2), (unsigned long long)nmiss);
+}
+
+// ---- the LDS cache's seeds -----------------------------------------------------------------
+// Seed i is the key of sample-table slot sslots[i] (igx_groupby_sort's top-E by count over a row
+// sample), looked up in the table's current generation (a key not there is no seed: seeds are
+// only ever found keys, never claimed).  Also records the generation they belong to.
+template <class L>
+__global__ __launch_bounds__(256) void k_gb_seeds(GbArgs a, const uint8_t *__restrict__ skrec, uint32_t skrec_len,
+                                                  const uint32_t *__restrict__ sslots, uint32_t nseeds,
+                                                  uint32_t *__restrict__ seeds, uint64_t *__restrict__ seed_gep) {
+    constexpr int KW = L::KW;
+    constexpr uint32_t KP = LdsCache<KW>::KP, KOFF = koff_of(KW);
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t gep = (uint32_t)*a.gen;
+    if (i == 0) *seed_gep = gep;
+    if (i >= nseeds) return;
+    uint32_t *out = seeds + (uint64_t)i * (KP + 4);
+    const uint32_t ss = sslots[i];
+    if (ss == 0xFFFFFFFFu) {   // fewer sampled keys than seeds
+        out[KP] = SLOT_OVF;
+        return;
+    }
+    uint32_t k[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) k[w] = reinterpret_cast<const uint32_t *>(skrec + (uint64_t)ss * skrec_len)[w];
+    const uint64_t h = hash_key<KW>(k);
+    const uint64_t tag = (h & ~EP_MAX) | gep;
+    uint32_t found = SLOT_OVF;
+    uint64_t s = home_slot(a, h);
+    for (uint32_t probe = 0; probe < a.max_probe; ++probe) {
+        const uint8_t *r = a.krec + s * a.krec_len;
+        const uint64_t t = *reinterpret_cast<const uint64_t *>(r + KOFF);
+        if ((t & EP_MAX) != gep) break;   // an empty slot of the generation: the key is not there
+        if (t == tag && ready_pub(*reinterpret_cast<const uint64_t *>(r + KOFF + 8), gep, a.ep)) {
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) eq = eq && reinterpret_cast<const uint32_t *>(r)[w] == k[w];
+            if (eq) {
+                found = (uint32_t)s;
+                break;
+            }
+        }
+        s = next_slot(a, s);
+    }
+#pragma unroll
+    for (uint32_t w = 0; w < KP; ++w) out[w] = (int)w < KW ? k[w] : 0u;
+    out[KP] = found;
+    out[KP + 1] = 0;
+    out[KP + 2] = (uint32_t)h;
+    out[KP + 3] = (uint32_t)(h >> 32);
 }
 
 // ---- direct form: no LDS cache ---------------------------------------------------------
@@ -1650,19 +1831,30 @@ __global__ __launch_bounds__(256) void k_slots_count(uint32_t *__restrict__ occ,
 // table's coherent pinned buffer (no copy after it): err block {bits, pad, LDS misses}, count
 // (then, released after them, the finalize's sequence number: the host polls it instead of
 // recording an event, whose release would flush L2 between finalize and the top-K)
-__device__ __forceinline__ void fin_export(const uint32_t *err, uint64_t total, uint64_t *host, uint64_t seq) {
+// It also closes the interval's books in the generation block: an interval that started its
+// generation holds every group as a claim (the key count is its group count), one that
+// continued adds its claims; a failed interval ends the generation.
+__device__ __forceinline__ void fin_export(const uint32_t *err, uint64_t total, uint64_t *host, uint64_t seq, uint64_t ep) {
     const uint64_t e0 = *reinterpret_cast<const volatile uint64_t *>(err);
     const uint64_t e1 = *reinterpret_cast<const volatile uint64_t *>(err + 2);
+    volatile uint64_t *gen = reinterpret_cast<volatile uint64_t *>(const_cast<uint32_t *>(err)) + GEN_WORD;
+    const bool fresh = gen[0] == ep;
+    const uint64_t claims = fresh ? total : gen[2];
+    const uint64_t keys = (uint32_t)e0 ? ~0ull : (fresh ? total : gen[1] + claims);
+    gen[1] = keys;
+    gen[2] = 0;
     __hip_atomic_store(host, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(host + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host + 4, claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host + 5, keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
     __hip_atomic_store(host + 3, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, uint64_t m, uint64_t *__restrict__ total,
                                                      const uint32_t *__restrict__ err, uint64_t *__restrict__ host,
-                                                     uint64_t seq) {
+                                                     uint64_t seq, uint64_t ep) {
     __shared__ uint32_t part[1024];
     const uint64_t per = (m + 1023) / 1024;
     const uint64_t b = threadIdx.x * per, e = min(m, b + per);
@@ -1684,7 +1876,7 @@ __global__ __launch_bounds__(1024) void k_slots_scan(uint32_t *__restrict__ v, u
     }
     if (threadIdx.x == 1023) {
         *total = part[1023];
-        fin_export(err, part[1023], host, seq);
+        fin_export(err, part[1023], host, seq, ep);
     }
 }
 
@@ -1696,7 +1888,7 @@ __global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ off, const uint32_t *__restrict__ cnt,
                                                      uint32_t *__restrict__ out, uint64_t *__restrict__ total,
                                                      const uint32_t *__restrict__ err, uint64_t *__restrict__ host,
-                                                     uint64_t seq) {
+                                                     uint64_t seq, uint64_t ep) {
     __shared__ uint32_t wsum[4], pre[4];
     __shared__ uint32_t buf[256 * 32];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1734,21 +1926,62 @@ __global__ __launch_bounds__(256) void k_slots_write(const uint32_t *__restrict_
     for (uint32_t j = threadIdx.x; j < tile_n; j += 256) out[base + j] = buf[j];
     if (!off && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
         *total = (uint64_t)base + tile_n;
-        fin_export(err, (uint64_t)base + tile_n, host, seq);
+        fin_export(err, (uint64_t)base + tile_n, host, seq, ep);
     }
 }
 
 // an interval's reset: the occupancy bitmap and the error block in one launch, and the byte
-// map when claims since the last finalize left bytes in it (nb16 of its 16-B quads, else 0)
+// map when claims since the last finalize left bytes in it (nb16 of its 16-B quads, else 0).
+// It also decides the interval's generation: with `may` (the host's part: the last interval
+// was finalized and this one is planned in the cached form) and the generation's keys within
+// `limit`, the generation goes on and the last interval's groups (groups[0 .. *ng), finalize's
+// slot list) get their value records back to first = UINT64_MAX, sums 0 (vq 16-B quads each);
+// otherwise this interval starts a generation at its own epoch.  Every thread reads the same
+// words (nothing in this launch writes gen[1] or the slot list), so all agree.
+struct ResetGen {
+    uint64_t *gen;            // the generation block (err words GEN_WORD..)
+    uint64_t ep, limit;
+    const uint32_t *groups;
+    const uint64_t *ng;
+    uint64_t *vrec;
+    uint32_t vw, may;         // value-record words (1 or an even number), the host's part
+};
 __global__ __launch_bounds__(256) void k_reset_clear(uint32_t *__restrict__ occ, uint64_t nwords,
                                                      uint32_t *__restrict__ err, uint4 *__restrict__ occb,
-                                                     uint64_t nb16) {
+                                                     uint64_t nb16, ResetGen rg) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
     const uint64_t n4 = nwords / 4;
-    for (uint64_t q = i; q < n4; q += (uint64_t)gridDim.x * 256) reinterpret_cast<uint4 *>(occ)[q] = make_uint4(0, 0, 0, 0);
-    for (uint64_t q = i; q < nb16; q += (uint64_t)gridDim.x * 256) occb[q] = make_uint4(0, 0, 0, 0);
+    for (uint64_t q = i; q < n4; q += stride) reinterpret_cast<uint4 *>(occ)[q] = make_uint4(0, 0, 0, 0);
+    for (uint64_t q = i; q < nb16; q += stride) occb[q] = make_uint4(0, 0, 0, 0);
     if (i < (nwords & 3)) occ[n4 * 4 + i] = 0;
     if (i < 4) err[i] = 0;
+    const bool cont = rg.may && rg.gen[1] <= rg.limit;
+    if (cont) {
+        // one lane per 16-B quad of a record, a record's quads in adjacent lanes: each record
+        // leaves as one store instruction's contiguous pieces (one write request per record, the
+        // claim stores' shape), not one request per quad of a lane writing its record alone
+        const uint64_t ng = *rg.ng;
+        const uint32_t vq = rg.vw == 1 ? 1u : rg.vw / 2;
+        for (uint64_t j = i; j < ng * vq; j += stride) {
+            const uint64_t g = j / vq;
+            const uint32_t q = (uint32_t)(j - g * vq);
+            uint64_t *v = rg.vrec + (uint64_t)rg.groups[g] * rg.vw;
+            if (rg.vw == 1) *v = ~0ull;
+            else reinterpret_cast<uint4 *>(v)[q] = q ? make_uint4(0, 0, 0, 0) : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0);
+        }
+    }
+    if (i == 0) {
+        if (!cont) rg.gen[0] = rg.ep;
+        rg.gen[2] = 0;
+    }
+}
+
+// the interval's planned generation did not hold (its first update runs the direct or the
+// partitioned form, which start their own): it starts a generation at its epoch
+__global__ void k_gen_restart(uint64_t *gen, uint64_t ep) {
+    gen[0] = ep;
+    gen[2] = 0;
 }
 
 // materialise selected groups as packed rows key | aggs | first (the Stats rows of
@@ -1817,6 +2050,19 @@ struct igx_table {
     bool occb_dirty = false;     // cached-form claims since the byte map was last folded / cleared
     uint64_t occ_words = 0;
     uint64_t ep = 0;             // current epoch (1..EP_MAX)
+    bool persist = true;         // keys outlive their interval (IGX_GB_PERSIST=0: every reset starts a generation)
+    bool fin_since_update = false;   // a finalize listed the groups after the last update
+    bool gen_planned = false;    // the reset let the interval continue the generation (device decides by key count)
+    bool seed_on = true;         // sample-seeded LDS cache for kept keys (IGX_GB_SEED=0: off)
+    igx_table *seed_tab = nullptr;   // the row sample's counting table
+    uint32_t *seeds = nullptr;   // seed records (device), nseeds of them
+    uint32_t *seed_slots = nullptr;  // the sample table's top-E slots (device)
+    uint64_t *seed_gep = nullptr;    // device: the generation the seeds were looked up in
+    uint32_t nseeds = 0, seeds_cap = 0;
+    uint32_t seed_left = 0;      // seeded intervals before the seeds are recomputed
+    bool interval_seeded = false;    // this interval's cached updates adopt the seeds
+    uint64_t claims_last = 0;    // the last collected finalize: keys its interval claimed
+    uint64_t gen_keys = 0;       // ... and the keys its generation held after it (~0: ended)
     uint64_t *n_groups = nullptr;
     uint64_t rows_fed = 0;       // rows given to update since the last reset
     bool prefer_sm = false;      // the last interval missed the LDS cache on most rows
@@ -1951,6 +2197,7 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMemsetAsync(t->krec, 0, ns * t->krec_len, ctx->stream);
     if (e == hipSuccess) e = hipMalloc(&t->vrec, ns * t->vrec_len);
     if (e == hipSuccess) e = hipMalloc(&t->err, 64);
+    if (e == hipSuccess) e = hipMemsetAsync(t->err, 0, 64, ctx->stream);
     if (e == hipSuccess) e = hipMalloc(&t->groups, ns * 4);
     if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 4);
     t->occ_words = (ns + 31) / 32;
@@ -1958,12 +2205,12 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
     if (e == hipSuccess) e = hipMalloc(&t->occb, t->occ_words * 32);
     if (e == hipSuccess) e = hipMemsetAsync(t->occb, 0, t->occ_words * 32, ctx->stream);
     if (e == hipSuccess) t->n_groups = reinterpret_cast<uint64_t *>(t->err + 4);   // behind the error block
-    if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 64);
+    if (e == hipSuccess) e = hipMalloc(&t->dbg_cnt, 256);
     if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void **>(&t->fin_host), 32, hipHostMallocMapped | hipHostMallocCoherent);
+        e = hipHostMalloc(reinterpret_cast<void **>(&t->fin_host), 64, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&t->fin_dev), t->fin_host, 0);
-    if (e == hipSuccess) std::fill(t->fin_host, t->fin_host + 4, 0ull);
-    if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream);
+    if (e == hipSuccess) std::fill(t->fin_host, t->fin_host + 8, 0ull);
+    if (e == hipSuccess) e = hipMemsetAsync(t->dbg_cnt, 0, 256, ctx->stream);
     if (e != hipSuccess) {
         igx_groupby_destroy(t);
         return igx_fail(ctx, IGX_ENOMEM, "groupby_create: %s", hipGetErrorString(e));
@@ -1973,6 +2220,8 @@ extern "C" int igx_groupby_create(igx_ctx *ctx, const uint32_t *key_widths, uint
         const unsigned long v = std::strtoul(m, nullptr, 0);
         if (v <= IGX_GB_PART) t->mode = (uint32_t)v;
     }
+    if (const char *m = std::getenv("IGX_GB_PERSIST")) t->persist = std::strtoul(m, nullptr, 0) != 0;   // A/B knob
+    if (const char *m = std::getenv("IGX_GB_SEED")) t->seed_on = std::strtoul(m, nullptr, 0) != 0;       // A/B knob
     *out = t;
     return igx_groupby_reset(t);
 }
@@ -1994,16 +2243,37 @@ extern "C" int igx_groupby_reset(igx_table *t) {
     t->fin_status = IGX_OK;
     // A new interval is a new epoch: records of older epochs read as empty and a claimer
     // initialises its value record, so only the bitmap and the error word are cleared.
+    bool wrapped = false;
     if (++t->ep > EP_MAX) {
         hipLaunchKernelGGL(k_table_clear, dim3(2048), dim3(256), 0, ctx->stream, t->krec, t->krec_len, t->koff,
                            t->nslots);
         IGX_HIP(ctx, hipGetLastError());
         t->ep = 1;
+        wrapped = true;
     }
+    // The generation goes on (the device checks its key count) when the last interval's groups
+    // were listed by a finalize after its last update and this interval is planned in the cached
+    // form (the direct and partitioned forms start their own: k_gen_restart if the plan changes).
+    ResetGen rg{};
+    rg.gen = reinterpret_cast<uint64_t *>(t->err) + GEN_WORD;
+    rg.ep = t->ep;
+    // the most keys a generation may hold after an interval: 4/5 of the slots (a 1 024-slot probe
+    // region then overflows only past 7 standard deviations of its expected fill)
+    const uint64_t fill = t->nslots / 5 * 4;
+    rg.limit = fill > t->cap ? fill - t->cap : 0;
+    rg.groups = t->groups;
+    rg.ng = t->n_groups;
+    rg.vrec = t->vrec;
+    rg.vw = t->vrec_len / 8;
+    const bool planned_cached = !(t->mode == IGX_GB_DIRECT || t->mode == IGX_GB_PART ||
+                                  (t->mode == IGX_GB_AUTO && t->direct_left > 0));
+    rg.may = t->persist && !wrapped && t->fin_since_update && rg.limit > 0 && planned_cached ? 1u : 0u;
+    t->gen_planned = rg.may != 0;
     // the bitmap, the error bits and the LDS-miss count (and the byte map if it holds claims)
     const uint64_t nb16 = t->occb_dirty ? t->occ_words * 2 : 0;
-    hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)std::min<uint64_t>(1024, (std::max(t->occ_words / 4, nb16) + 255) / 256 + 1)),
-                       dim3(256), 0, ctx->stream, t->occ, t->occ_words, t->err, reinterpret_cast<uint4 *>(t->occb), nb16);
+    const uint64_t grid = rg.may ? 1024 : std::min<uint64_t>(1024, (std::max(t->occ_words / 4, nb16) + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)grid), dim3(256), 0, ctx->stream, t->occ, t->occ_words, t->err,
+                       reinterpret_cast<uint4 *>(t->occb), nb16, rg);
     t->occb_dirty = false;
     IGX_HIP(ctx, hipGetLastError());
     t->rows_fed = 0;
@@ -2022,6 +2292,10 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->occ);
     (void)hipFree(t->occb);
     (void)hipFree(t->dbg_cnt);
+    (void)hipFree(t->seeds);
+    (void)hipFree(t->seed_slots);
+    (void)hipFree(t->seed_gep);
+    if (t->seed_tab) igx_groupby_destroy(t->seed_tab);
     (void)hipFree(t->p_recs);
     (void)hipFree(t->p_cnt);
     (void)hipFree(t->p_mask);
@@ -2041,6 +2315,19 @@ constexpr uint64_t MORE_PROBERS_ON_PM = 390;
 constexpr uint64_t MORE_PROBERS_OFF_PM = 370;
 constexpr uint32_t DIRECT_RUN = 16;             // ... for this many intervals
 
+// the cached kernel's LDS cache entries (E) for naggs aggregates in its NA-slot variant
+template <class L, int NA>
+static uint32_t gb_entries(uint32_t naggs) {
+    const size_t entry = 4 + 4 + 8 + 8 * naggs + 4 * LdsCache<L::KW>::KP;
+    const size_t rings = ARING * 16 + MRING * (16 * MissRing<L::KW, NA>::EQ + 4) + GHOST * 4;
+    const size_t budget = GB_LDS_TOTAL - rings;
+    return 8 * (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, budget / (8 * entry)));
+}
+template <class L>
+static uint32_t gb_entries_for(uint32_t naggs) {
+    return naggs <= 2 ? gb_entries<L, 2>(naggs) : gb_entries<L, AMAX>(naggs);
+}
+
 template <class L, bool DBG, int NA>
 static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     static bool attr = false;
@@ -2051,9 +2338,7 @@ static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     }
     const size_t entry = 4 + 4 + 8 + 8 * a.naggs + 4 * LdsCache<L::KW>::KP;
     const size_t rings = ARING * 16 + MRING * (16 * MissRing<L::KW, NA>::EQ + 4) + GHOST * 4;
-    const size_t budget = GB_LDS_TOTAL - rings;
-    const uint32_t nsets = (uint32_t)std::max<size_t>(1, std::min<size_t>(1024, budget / (8 * entry)));
-    const uint32_t E = 8 * nsets;
+    const uint32_t E = gb_entries<L, NA>(a.naggs);
     a.lds_entries = E;
     const size_t lds = E * entry + rings;
     hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), lds, ctx->stream, a);
@@ -2386,6 +2671,105 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
     return launch_part_as<L, PNV>(t, ctx, a, p, region);
 }
 
+// The sample-seeded LDS cache (tools/cache_sim.py: C2 33.7 -> 31.2 % misses, C5 45.4
+// -> 42.6 %, against 30.7 / 42.2 % for an ideal top-E cache).  The first SEED_SAMPLE rows of the
+// interval's first update are counted by key in a scratch table (the cached kernel itself, with
+// one COUNT aggregate), its top-E groups by count are selected on the device (igx_groupby_sort),
+// and k_gb_seeds looks each of them up in the table's current generation.  Every workgroup of the
+// interval's cached updates adopts the found ones before its stream starts.  Hot keys of a
+// stream are stable, so the seeds are recomputed every SEED_EVERY seeded intervals (and after a
+// generation ended); seeds of another generation are never adopted (the kernel compares).
+constexpr uint32_t SEED_EVERY = 8;
+constexpr uint64_t SEED_MIN_ROWS = 8u << 20;    // smaller updates: no seeds (IGX_GB_SEED_MIN overrides)
+constexpr uint64_t SEED_SAMPLE = 1u << 20;      // sampled rows: max(1M, rows / 64)
+
+template <class L>
+static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
+    const uint32_t E = gb_entries_for<L>(t->naggs);
+    const uint64_t S = std::min<uint64_t>(a.n, std::max<uint64_t>(SEED_SAMPLE, a.n / 64));
+    if (t->seed_tab && t->seed_tab->cap < S) {
+        igx_groupby_destroy(t->seed_tab);
+        t->seed_tab = nullptr;
+    }
+    if (!t->seed_tab) {
+        igx_agg cnt{};
+        cnt.kind = IGX_AGG_COUNT;
+        cnt.col = IGX_NO_COL;
+        cnt.cond_col = IGX_NO_COL;
+        cnt.out_width = 8;
+        igx_table *st = nullptr;
+        int rc = igx_groupby_create(ctx, t->key_widths, t->nkeys, &cnt, 1, std::max<uint64_t>(S, 4ull * E), &st);
+        if (rc) return rc;
+        st->persist = false;
+        st->seed_on = false;
+        st->mode = IGX_GB_CACHED;
+        t->seed_tab = st;
+    }
+    if (t->seeds_cap < E) {
+        (void)hipFree(t->seeds);
+        (void)hipFree(t->seed_slots);
+        t->seeds = nullptr;
+        t->seed_slots = nullptr;
+        t->seeds_cap = 0;
+        IGX_HIP(ctx, hipMalloc(&t->seeds, (size_t)E * (LdsCache<L::KW>::KP + 4) * 4));
+        IGX_HIP(ctx, hipMalloc(&t->seed_slots, (size_t)E * 4));
+        if (!t->seed_gep) IGX_HIP(ctx, hipMalloc(&t->seed_gep, 8));
+        t->seeds_cap = E;
+    }
+    igx_table *st = t->seed_tab;
+    (void)fin_collect(st, nullptr);   // the last sample's read-back (landed long ago)
+    st->fin_status = IGX_OK;
+    (void)igx_groupby_reset(st);
+    // the same columns and fused predicates, the sample's rows, one COUNT into the sample table
+    // (aggregate 0's columns are still loaded: predicates and guards may read their raw values)
+    GbArgs b = a;
+    b.n = S;
+    b.naggs = 1;
+    b.vcount[0] = 1;
+    b.hascond[0] = 0;
+    b.krec = st->krec;
+    b.vrec = st->vrec;
+    b.krec_len = st->krec_len;
+    b.krec_total = (uint32_t)(st->nslots * st->krec_len);
+    b.vrec_words = st->vrec_len / 8;
+    b.vrec_total = st->nslots * st->vrec_len < (1ull << 32) ? (uint32_t)(st->nslots * st->vrec_len) : 0u;
+    b.err = st->err;
+    b.occ = st->occ;
+    b.occb = st->occb;
+    b.ep = st->ep;
+    b.gen = reinterpret_cast<uint64_t *>(st->err) + GEN_WORD;
+    b.sshift = 64 - st->sbits;
+    b.rmask = (1ull << st->rbits) - 1;
+    b.max_probe = 1u << st->rbits;
+    b.dbg = 0;
+    b.sm = 0;
+    b.direct = 0;
+    b.nl = NL_DEFAULT;
+    b.seeds = nullptr;
+    b.seed_gep = nullptr;
+    b.nseeds = 0;
+    b.dbg_cnt = st->dbg_cnt;
+    st->rows_fed = S;
+    st->fin_since_update = false;
+    st->interval_direct = st->interval_part = false;
+    st->occb_dirty = true;
+    launch_gb<L>(ctx, b, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((S + GTB - 1) / GTB, (uint64_t)ctx->num_cus)));
+    IGX_HIP(ctx, hipGetLastError());
+    int rc = igx_groupby_finalize_async(st, nullptr);
+    if (rc) return rc;
+    igx_tsortkey key{};
+    key.src = IGX_TSRC_AGG;
+    key.index = 0;
+    key.desc = 1;
+    rc = igx_groupby_sort(st, &key, 1, E, t->seed_slots);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gb_seeds<L>, dim3((E + 255) / 256), dim3(256), 0, ctx->stream, a, st->krec, st->krec_len,
+                       t->seed_slots, E, t->seeds, t->seed_gep);
+    IGX_HIP(ctx, hipGetLastError());
+    t->nseeds = E;
+    return IGX_OK;
+}
+
 // one update over layout L in the interval's form
 template <class L>
 static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
@@ -2412,6 +2796,24 @@ static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
         launch_direct<L>(ctx, a);
     } else {
         t->occb_dirty = true;   // the cached form's claims mark the byte map
+        if (t->rows_fed == a.n) {   // the interval's first update decides whether it is seeded
+            uint64_t min_rows = SEED_MIN_ROWS;
+            if (const char *m = std::getenv("IGX_GB_SEED_MIN")) min_rows = std::strtoull(m, nullptr, 0);
+            t->interval_seeded = false;
+            if (t->seed_on && t->gen_planned && !a.dbg && a.n >= min_rows) {
+                if (t->seed_left == 0 || !t->nseeds) {
+                    if (seeds_compute<L>(t, ctx, a) == IGX_OK) t->seed_left = SEED_EVERY;
+                    else t->nseeds = 0;   // no seeds this time (the sample table failed): plain cache
+                }
+                --t->seed_left;
+                t->interval_seeded = t->nseeds > 0;
+            }
+        }
+        if (t->interval_seeded) {
+            a.seeds = t->seeds;
+            a.seed_gep = t->seed_gep;
+            a.nseeds = t->nseeds;
+        }
         launch_gb<L>(ctx, a, blocks);
     }
     return IGX_OK;
@@ -2438,9 +2840,10 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     if (nrows == 0) return IGX_OK;
     if (!cols || !key_cols) return igx_fail(ctx, IGX_EINVAL, "groupby_update: null columns");
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "groupby_update: more than 2^32 rows in one call");
-    if (base_idx + nrows > READY_IDX)   // `ready` carries first_ins + 1 in 48 bits
+    if (base_idx + nrows >= READY_IDX)   // `ready` carries first_ins + 1 (a kept key's: index + 2) in 48 bits
         return igx_fail(ctx, IGX_EINVAL, "groupby_update: event indices reach 2^48 (rebase the interval's indices)");
     t->rows_fed += nrows;
+    t->fin_since_update = false;
     GbArgs a{};
     uint32_t w = 0;
     for (uint32_t k = 0; k < t->nkeys; ++k) {
@@ -2646,6 +3049,7 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
     a.occ = t->occ;
     a.occb = t->occb;
     a.ep = t->ep;
+    a.gen = reinterpret_cast<uint64_t *>(t->err) + GEN_WORD;
     a.sshift = 64 - t->sbits;
     a.rmask = (1ull << t->rbits) - 1;
     a.max_probe = 1u << t->rbits;
@@ -2680,6 +3084,11 @@ extern "C" int igx_groupby_update_ex(igx_table *t, const igx_col *cols, uint32_t
         if (t->region_off > 0) --t->region_off;
     }
     if (std::getenv("IGX_GB_DEBUG")) t->interval_direct = t->interval_part = false;   // diagnostics: cached form
+    if (t->gen_planned && (t->interval_direct || t->interval_part)) {
+        hipLaunchKernelGGL(k_gen_restart, dim3(1), dim3(1), 0, ctx->stream, a.gen, t->ep);
+        IGX_HIP(ctx, hipGetLastError());
+        t->gen_planned = false;
+    }
     int rc = IGX_OK;
 #ifdef IGX_DEV_FAST   // development builds: the bench's key layouts only (fast kernel iteration)
     if (layout_is<TcpKey>(kw, t->nkeys)) rc = launch_form<TcpKey>(t, ctx, a, blocks);
@@ -2727,6 +3136,7 @@ static int fin_launch(igx_table *t) {
     hipLaunchKernelGGL(k_slots_count, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
                        t->tile_cnt, t->occb_dirty ? t->occb : (uint8_t *)nullptr);
     t->occb_dirty = false;
+    t->fin_since_update = true;
     // the kernel that finds the group count also writes the read-back into fin_host
     const uint64_t seq = ++t->fin_seq;
     t->fin_snap.rows_fed = t->rows_fed;
@@ -2737,12 +3147,12 @@ static int fin_launch(igx_table *t) {
     t->fin_snap.sampled = t->probe_rows;
     if (tiles <= SLOTS_INLINE_TILES) {
         hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
-                           (const uint32_t *)nullptr, t->tile_cnt, t->groups, t->n_groups, t->err, t->fin_dev, seq);
+                           (const uint32_t *)nullptr, t->tile_cnt, t->groups, t->n_groups, t->err, t->fin_dev, seq, t->ep);
     } else {
         hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(1024), 0, ctx->stream, t->tile_cnt, tiles, t->n_groups, t->err,
-                           t->fin_dev, seq);
+                           t->fin_dev, seq, t->ep);
         hipLaunchKernelGGL(k_slots_write, dim3((unsigned)tiles), dim3(256), 0, ctx->stream, t->occ, t->occ_words,
-                           t->tile_cnt, (const uint32_t *)nullptr, t->groups, (uint64_t *)nullptr, t->err, t->fin_dev, seq);
+                           t->tile_cnt, (const uint32_t *)nullptr, t->groups, (uint64_t *)nullptr, t->err, t->fin_dev, seq, t->ep);
     }
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
@@ -2772,6 +3182,9 @@ static int fin_apply(igx_table *t) {
     const uint64_t misses = h[1];
     const uint64_t ng = h[2];
     const uint32_t spilled = reinterpret_cast<const uint32_t *>(h)[1];   // a region overflowed
+    t->claims_last = h[4];
+    t->gen_keys = h[5];
+    if (h[4] == ng || h[5] == ~0ull) t->seed_left = 0;   // a generation started or ended: fresh seeds
     const auto &f = t->fin_snap;   // the interval this read-back belongs to
     if (spilled && f.region) t->region_off = DIRECT_RUN + 1;
     t->host_groups = ng;
@@ -2881,6 +3294,9 @@ extern "C" int igx_groupby_info(igx_table *t, igx_groupby_info_t *out) {
     out->loaders = t->more_probers ? NL_DEFAULT - 1 : NL_DEFAULT;
     out->miss_permille = t->miss_pm;
     out->rows = t->rows_fed;
+    out->claims = t->claims_last;
+    out->gen_keys = t->gen_keys;
+    out->persist = t->persist ? 1u : 0u;
     return IGX_OK;
 }
 
@@ -2986,11 +3402,11 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.
-extern "C" int igx_groupby_debug_counts(igx_table *t, uint64_t *out8) {
-    if (!t || !out8) return IGX_EINVAL;
+extern "C" int igx_groupby_debug_counts(igx_table *t, uint64_t *out16) {   // out16: 32 words
+    if (!t || !out16) return IGX_EINVAL;
     igx_ctx *ctx = t->ctx;
-    IGX_HIP(ctx, hipMemcpyAsync(out8, t->dbg_cnt, 64, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipMemcpyAsync(out16, t->dbg_cnt, 256, hipMemcpyDeviceToHost, ctx->stream));
     IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    IGX_HIP(ctx, hipMemsetAsync(t->dbg_cnt, 0, 64, ctx->stream));
+    IGX_HIP(ctx, hipMemsetAsync(t->dbg_cnt, 0, 256, ctx->stream));
     return IGX_OK;
 }

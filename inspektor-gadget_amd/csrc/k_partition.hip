@@ -116,6 +116,144 @@ __global__ __launch_bounds__(PTB) void k_part_scatter(const uint8_t *__restrict_
     }
 }
 
+// ---- the same partition straight from a finalized table (igx_partition_groups) ---------
+// The rows are the table's groups -- key words | aggregates masked to their out_width | first
+// index, igx_groupby_gather's layout -- read through the slot list, and their number is the
+// group count on the device, so an asynchronously finalized table is partitioned without a
+// host round trip: both passes size their chunks from that count.
+struct GroupSrc {
+    const uint8_t *keys, *vals;
+    const uint32_t *groups;
+    const uint64_t *ng;
+    uint64_t cap;                 // rows the output holds
+    uint32_t key_stride, val_stride, key_words, naggs;
+    uint32_t m[16];               // (lo, hi) masks per aggregate
+};
+
+__device__ __forceinline__ uint64_t src_rows(const GroupSrc &g) { return min(*g.ng, g.cap); }
+
+__device__ __forceinline__ uint32_t src_word(const GroupSrc &g, uint32_t slot, uint32_t w) {
+    if (w < g.key_words) return reinterpret_cast<const uint32_t *>(g.keys + (uint64_t)slot * g.key_stride)[w];
+    const uint32_t *v = reinterpret_cast<const uint32_t *>(g.vals + (uint64_t)slot * g.val_stride);
+    const uint32_t a = w - g.key_words;
+    return a < 2 * g.naggs ? v[2 + a] & g.m[a] : v[a - 2 * g.naggs];
+}
+
+// The owner of every row, computed once: each thread takes GH rows at a time, their slots
+// first, then their keys' first words, so GH scattered key reads are in flight at once (a
+// dependent slot -> key -> owner chain per row left the pass latency-bound); owners go to a byte
+// array the scatter reads back in order.
+constexpr int GH = 4;
+constexpr uint32_t GKW = 8;   // key words loaded up front (longer keys read the rest in a loop)
+
+__global__ __launch_bounds__(PTB) void k_gpart_hist(GroupSrc g, uint32_t nparts, uint32_t *__restrict__ hist,
+                                                    uint8_t *__restrict__ owner) {
+    __shared__ uint32_t cnt[PMAXP];
+    if (threadIdx.x < PMAXP) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t n = src_rows(g), chunk = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = min(n, (uint64_t)blockIdx.x * chunk), b1 = min(n, b0 + chunk);
+    for (uint64_t r0 = b0 + threadIdx.x; r0 < b1; r0 += GH * PTB) {
+        uint32_t slot[GH];
+#pragma unroll
+        for (int u = 0; u < GH; ++u) {
+            const uint64_t r = r0 + (uint64_t)u * PTB;
+            slot[u] = r < b1 ? g.groups[r] : 0u;
+        }
+        uint32_t kw[GH][GKW];
+#pragma unroll
+        for (int u = 0; u < GH; ++u) {
+            const uint32_t *k = reinterpret_cast<const uint32_t *>(g.keys + (uint64_t)slot[u] * g.key_stride);
+#pragma unroll
+            for (uint32_t w = 0; w < GKW; ++w) kw[u][w] = w < g.key_words ? k[w] : 0u;
+        }
+        uint32_t o[GH];
+#pragma unroll
+        for (int u = 0; u < GH; ++u) {   // FNV-1a over the key words: row_owner's function
+            const uint32_t *k = reinterpret_cast<const uint32_t *>(g.keys + (uint64_t)slot[u] * g.key_stride);
+            uint32_t h = 0x811C9DC5u;
+#pragma unroll
+            for (uint32_t w = 0; w < GKW; ++w)
+                if (w < g.key_words) h = (h ^ kw[u][w]) * 16777619u;
+            for (uint32_t w = GKW; w < g.key_words; ++w) h = (h ^ k[w]) * 16777619u;
+            o[u] = h % nparts;
+        }
+#pragma unroll
+        for (int u = 0; u < GH; ++u) {
+            const uint64_t r = r0 + (uint64_t)u * PTB;
+            if (r < b1) {
+                atomicAdd(&cnt[o[u]], 1u);
+                owner[r] = (uint8_t)o[u];
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// k_part_scatter's wave / LDS ranking over the table's rows; a row's words are written by
+// consecutive lanes of one store (one lane per word, rows of a wave side by side)
+__global__ __launch_bounds__(PTB) void k_gpart_scatter(GroupSrc g, uint32_t nparts, const uint32_t *__restrict__ off,
+                                                       const uint8_t *__restrict__ owner, uint8_t *__restrict__ out) {
+    __shared__ uint32_t base[PMAXP];
+    __shared__ uint32_t wcnt[PTB / 64][PMAXP];
+    __shared__ uint32_t dst_slot[PTB][2];         // per row of the tile: output row, table slot
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t row_words = g.key_words + 2 * g.naggs + 2;
+    if (threadIdx.x < nparts) base[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+    const uint64_t n = src_rows(g), chunk = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = min(n, (uint64_t)blockIdx.x * chunk), b1 = min(n, b0 + chunk);
+    for (uint64_t t0 = b0; t0 < b1; t0 += PTB) {
+        for (uint32_t i = threadIdx.x; i < (PTB / 64) * PMAXP; i += PTB) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t r = t0 + threadIdx.x;
+        const bool in = r < b1;
+        const uint32_t slot = in ? g.groups[r] : 0u;
+        const uint32_t o = in ? (uint32_t)owner[r] : 0xFFFFFFFFu;
+        uint32_t rank = 0;
+        uint64_t todo = __ballot(in);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__ffsll((long long)todo) - 1;
+            const uint32_t lo = __shfl(o, (int)leader);
+            const uint64_t m = __ballot(o == lo);
+            if (o == lo) rank = (uint32_t)__popcll(m & lanemask_lt());
+            if (lane == 0) wcnt[wave][lo] = (uint32_t)__popcll(m);
+            todo &= ~m;
+        }
+        __syncthreads();
+        if (in) {
+            uint32_t before = 0;
+            for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][o];
+            dst_slot[threadIdx.x][0] = base[o] + before + rank;
+            dst_slot[threadIdx.x][1] = slot;
+        }
+        __syncthreads();
+        // one lane per output word, 8 words in flight per lane (their loads before any store)
+        const uint32_t tile = (uint32_t)min<uint64_t>(PTB, b1 - t0), words = tile * row_words;
+        for (uint32_t i0 = threadIdx.x; i0 < words; i0 += 8 * PTB) {
+            uint32_t v[8];
+            uint64_t d[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t i = i0 + u * PTB;
+                const uint32_t j = i / row_words, w = i - j * row_words;
+                d[u] = i < words ? (uint64_t)dst_slot[j][0] * row_words + w : ~0ull;
+                v[u] = i < words ? src_word(g, dst_slot[j][1], w) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (d[u] != ~0ull) reinterpret_cast<uint32_t *>(out)[d[u]] = v[u];
+        }
+        __syncthreads();
+        if (threadIdx.x < nparts) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < PTB / 64; ++w) tot += wcnt[w][threadIdx.x];
+            base[threadIdx.x] += tot;
+        }
+        __syncthreads();
+    }
+}
+
 // ---- AoS -> SoA -----------------------------------------------------------------------
 struct IngestArgs {
     const uint8_t *rec;
@@ -179,6 +317,52 @@ extern "C" int igx_partition_rows(igx_ctx *ctx, const uint8_t *rows, uint64_t nr
                        part_counts);
     hipLaunchKernelGGL(k_part_scatter, dim3(nblocks), dim3(PTB), 0, ctx->stream, rows, nrows, row_bytes, kw, nparts,
                        chunk, hist, out);
+    IGX_HIP(ctx, hipGetLastError());
+    return IGX_OK;
+}
+
+extern "C" int igx_partition_groups(igx_ctx *ctx, const igx_table_view *view, const uint32_t *out_widths,
+                                    uint32_t nparts, uint8_t *out, uint64_t cap_rows, uint64_t *part_counts) {
+    if (!ctx) return IGX_EINVAL;
+    if (!view || !part_counts) return igx_fail(ctx, IGX_EINVAL, "partition_groups: null argument");
+    if (nparts == 0 || nparts > PMAXP) return igx_fail(ctx, IGX_EINVAL, "partition_groups: nparts must be 1..%u", PMAXP);
+    if (view->naggs > 8 || view->key_bytes % 4 || !view->groups || !view->d_n_groups || !view->keys ||
+        !view->first_idx)
+        return igx_fail(ctx, IGX_EINVAL, "partition_groups: not a finalized table view");
+    if (cap_rows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "partition_groups: more than 2^32 rows");
+    if (cap_rows == 0) {
+        IGX_HIP(ctx, hipMemsetAsync(part_counts, 0, nparts * sizeof(uint64_t), ctx->stream));
+        return IGX_OK;
+    }
+    if (!out || (reinterpret_cast<uintptr_t>(out) & 3)) return igx_fail(ctx, IGX_EINVAL, "partition_groups: out");
+    GroupSrc g{};
+    g.keys = view->keys;
+    g.vals = reinterpret_cast<const uint8_t *>(view->first_idx);
+    g.groups = view->groups;
+    g.ng = view->d_n_groups;
+    g.cap = cap_rows;
+    g.key_stride = view->key_stride;
+    g.val_stride = view->val_stride;
+    g.key_words = view->key_bytes / 4;
+    g.naggs = view->naggs;
+    for (uint32_t x = 0; x < view->naggs; ++x) {
+        const uint32_t ow = out_widths ? out_widths[x] : 8;
+        const uint64_t m = (ow == 0 || ow >= 8) ? ~0ull : ((1ull << (8 * ow)) - 1);
+        g.m[2 * x] = (uint32_t)m;
+        g.m[2 * x + 1] = (uint32_t)(m >> 32);
+    }
+    // blocks: as igx_partition_rows would pick for the most rows the output holds
+    const uint32_t nblocks = (uint32_t)std::min<uint64_t>(std::max(1, ctx->num_cus * 2), (cap_rows + PTB - 1) / PTB);
+    void *scratch;
+    const size_t hist_b = igx_align((size_t)nparts * nblocks * 4, 256);
+    int rc = igx_scratch(ctx, hist_b + cap_rows, &scratch);
+    if (rc) return rc;
+    uint32_t *hist = static_cast<uint32_t *>(scratch);
+    uint8_t *owner = static_cast<uint8_t *>(scratch) + hist_b;   // each row's owner, from the first pass
+    hipLaunchKernelGGL(k_gpart_hist, dim3(nblocks), dim3(PTB), 0, ctx->stream, g, nparts, hist, owner);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PTB), 0, ctx->stream, hist, nparts * nblocks, nparts, nblocks,
+                       part_counts);
+    hipLaunchKernelGGL(k_gpart_scatter, dim3(nblocks), dim3(PTB), 0, ctx->stream, g, nparts, hist, owner, out);
     IGX_HIP(ctx, hipGetLastError());
     return IGX_OK;
 }

@@ -1856,12 +1856,18 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                 const size_t lds = ((size_t)da.d.cap * da.d.nw + DICT_MAXD) * 4;
                 static bool attr = false;
                 if (!attr) {
-                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_dict_rank),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)((DICT_LDS_WORDS + DICT_MAXD) * 4));
+                    // up to 80 KB of dynamic LDS (gfx950's 160 KB per CU holds it); a refused
+                    // attribute fails the sort here rather than letting k_compose read stale ranks
+                    const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void *>(k_dict_rank),
+                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                              (int)((DICT_LDS_WORDS + DICT_MAXD) * 4));
+                    if (ae != hipSuccess) return igx_fail(ctx, IGX_EIO, "sort: k_dict_rank LDS: %s", hipGetErrorString(ae));
                     attr = true;
                 }
                 hipLaunchKernelGGL(k_dict_rank, dim3(1), dim3(1024), lds, ctx->stream, da.d);
+                // a launch that did not start leaves the ranks unwritten: fail instead of composing them
+                if (const hipError_t le = hipGetLastError(); le != hipSuccess)
+                    return igx_fail(ctx, IGX_EIO, "sort: k_dict_rank launch: %s", hipGetErrorString(le));
             }
         }
         if (u64_shape) {

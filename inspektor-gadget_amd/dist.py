@@ -235,15 +235,15 @@ def shutdown():
     _comm = None
 
 
-def allreduce_hist(hist):
-    """C3: in-place sum of a u32 histogram over ranks."""
-    c = comm()
+def allreduce_hist(hist, c=None):
+    """C3: in-place sum of a u32 histogram over ranks (c: a transport; default comm())."""
+    c = c or comm()
     return hist if c is None else c.allreduce_u32(hist)
 
 
-def allgather_rows(rows):
+def allgather_rows(rows, c=None):
     """Concatenate every rank's (n_r, row_bytes) uint8 rows in rank order (n_r may differ)."""
-    c = comm()
+    c = c or comm()
     return rows if c is None else c.allgather_rows(rows)
 
 
@@ -254,11 +254,21 @@ def partition_by_owner(rows, key_bytes, ws):
     return engine.partition_rows(rows, key_bytes, ws)
 
 
-def exchange_partitioned(rows, counts):
+def exchange_partitioned(rows, counts, c=None):
     """All-to-all of rows already grouped by destination rank (counts[r] rows for rank r,
-    in rank order).  Returns the rows this rank owns, in source-rank order."""
-    c = comm()
+    in rank order; rows past their sum are ignored).  Returns the rows this rank owns, in
+    source-rank order."""
+    c = c or comm()
+    rows = rows[:sum(counts)]
     return rows if c is None else c.alltoallv_rows(rows, counts)
+
+
+def owner_capacity(capacity, ws, slack=1.25):
+    """Groups an owner table must hold when `capacity` bounds the distinct keys of the whole
+    (global) interval: keys reach their owner by a hash of the key, so an owner holds about
+    1/ws of them; slack covers the hash's imbalance (at 1M keys per owner its spread is
+    ~0.1 %)."""
+    return min(capacity, int(capacity * slack / ws) + 4096)
 
 
 def exchange_rows(rows, key_bytes):
@@ -286,11 +296,12 @@ def unpack_rows(rows, key_widths, naggs):
     return cols, aggs, first
 
 
-def merge_partials(rows, key_widths, out_widths, capacity, table=None):
+def merge_partials(rows, key_widths, out_widths, capacity, table=None, sync=True):
     """Owner-side merge of exchanged partial groups on the device: one igx table whose
     aggregates SUM the partials and whose first index is the MIN of the partials' (the
     rows' u64 first column drives igx_groupby_update_ex's index column).  Returns the
-    engine.Table, finalized (`table`, when given, is reset and reused)."""
+    engine.Table, finalized (`table`, when given, is reset and reused; sync=False leaves the
+    group count on the device, igx_groupby_finalize_async)."""
     from . import _abi, engine
     kcols, aggs, first = unpack_rows(rows, key_widths, len(out_widths))
     nk = len(kcols)
@@ -302,17 +313,17 @@ def merge_partials(rows, key_widths, out_widths, capacity, table=None):
     n = rows.shape[0]
     if n:
         table.update(kcols + aggs + [first], list(range(nk)), n, 0, idx_col=nk + len(aggs))
-    table.finalize()
+    table.finalize(sync=sync)
     return table
 
 
-def merge_topk(cand, key_bytes, naggs, sort_keys, k):
+def merge_topk(cand, key_bytes, naggs, sort_keys, k, c=None):
     """Exact global top-K from all ranks' candidate rows (key | aggs | first): all-gather,
     then igx_topk with the global first index as the position.  sort_keys:
     [(agg_index, desc)] in sortBy order."""
     from . import engine
     torch = torch_mod()
-    allc = allgather_rows(cand)
+    allc = allgather_rows(cand, c)
     if allc.shape[0] == 0:
         return allc
     o = key_bytes

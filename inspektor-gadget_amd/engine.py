@@ -225,6 +225,7 @@ class Table:
         self.h = h
         self.key_widths = list(key_widths)
         self.naggs = len(aggs)
+        self.out_widths = [int(a.out_width) or 8 for a in aggs]
         self.capacity = capacity
 
     def update(self, cols, key_cols, n, base_idx=0, preds=(), valid=None, idx_col=None):
@@ -272,6 +273,7 @@ class Table:
             self.ctx.check(self.ctx.L.igx_groupby_finalize(self.h, C.byref(v)))
         else:
             self.ctx.check(self.ctx.L.igx_groupby_finalize_async(self.h, C.byref(v)))
+        self._view = v
         self.fin = {"n_groups": v.n_groups if sync else None, "n_slots": v.n_slots, "key_bytes": v.key_bytes,
                     "key_stride": v.key_stride, "val_stride": v.val_stride, "keys_ptr": v.keys,
                     "aggs_ptr": [v.aggs[i] for i in range(v.naggs)], "first_ptr": v.first_idx,
@@ -316,6 +318,28 @@ class Table:
         if k:
             self.ctx.check(self.ctx.L.igx_groupby_gather(self.h, ptr(slots), k, ptr(out)))
         return out[:k]
+
+    def partition(self, nparts, out_widths=None):
+        """igx_partition_groups: the finalized table's groups as packed rows (key | aggregates
+        wrapped to out_widths | first index), grouped by owner part (FNV-1a over the key words
+        mod nparts, as igx_partition_rows), stable in slot order within a part -- the sender
+        side of the owner exchange, with the group count read on the device (works after
+        finalize(sync=False)).  Returns (rows (capacity, row_bytes) u8, counts (nparts,) i64),
+        both on the device; rows past the counts' sum are unused."""
+        torch = torch_mod()
+        ctx = self.ctx
+        ctx.bind_stream()
+        fin = self.fin
+        rb = fin["key_bytes"] + 8 * self.naggs + 8
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf = getattr(self, "_part_buf", None)
+        if buf is None or buf.shape != (self.capacity, rb):
+            buf = self._part_buf = torch.empty((max(1, self.capacity), rb), dtype=torch.uint8, device=dev)
+        cnt = torch.empty(nparts, dtype=torch.int64, device=dev)
+        ow = (C.c_uint32 * max(1, self.naggs))(*(out_widths or self.out_widths))
+        ctx.check(ctx.L.igx_partition_groups(ctx.h, C.byref(self._view), ow, nparts, ptr(buf), self.capacity,
+                                             ptr(cnt)))
+        return buf, cnt
 
     def destroy(self):
         if self.h:

@@ -61,17 +61,29 @@ def main():
             e0.record()
             tab.update(cols, list(range(nkey)), N, 0)
             e1.record()
+            if not a.noreset:
+                tab.finalize()   # lists the groups: the next reset keeps the keys (a generation)
             torch.cuda.synchronize()
             res.setdefault(v, []).append(e0.elapsed_time(e1))
-            if v & (8 | 65536):
-                cnt = (C.c_uint64 * 8)()
+            if v & (8 | 65536 | 262144):
+                cnt = (C.c_uint64 * 32)()
                 tab.ctx.check(tab.ctx.L.igx_groupby_debug_counts(tab.h, cnt))
                 if v & 8:
                     res.setdefault("hits_misses", []).append([cnt[0], cnt[1]])
                 if v & 65536:
                     res.setdefault("waits_lfull_pempty_ufull_sidle", []).append([cnt[4], cnt[5], cnt[6], cnt[7]])
+                if v & 262144:
+                    res.setdefault("atomics", []).append(
+                        {"server_updates": cnt[8], "server_minima": cnt[9], "server_record_requests": cnt[10],
+                         "server_line_requests": cnt[11], "server_straddles": cnt[12], "flush_updates": cnt[16],
+                         "flush_record_requests": cnt[18], "flush_minima": cnt[20],
+                         "claims": tab.info()["claims"]})
     os.environ.pop("IGX_GB_DEBUG", None)
-    out = {str(k): (float(np.median(v)) if not isinstance(k, str) else v[-1]) for k, v in res.items()}
+    out = {str(k): (float(np.median(v)) if not isinstance(k, str) else (v if k.startswith("atomics") else v[-1]))
+           for k, v in res.items()}
+    out["launch_ms"] = {str(k): v for k, v in res.items() if not isinstance(k, str)}
+    if hasattr(tab, "info"):
+        out["claims_last"] = tab.info()["claims"]
     out.update({"events": N, "keys": G, "zipf": a.zipf, "layout": a.layout, "noreset": a.noreset})
     print(json.dumps(out))
     tab.destroy()
