@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 METRIC = "events aggregated/sec (filter+group-by+top-K) at 1/2/4/8 MI355X; % HBM peak"   # BASELINE.json
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 EV_BYTES = 71                  # saddr16 daddr16 mntns8 pid4 comm16 lport2 dport2 family2 size4 dir1
 GROUP_BYTES = 90               # key 66 + sent 8 + recv 8 + first_idx 8
 TCP_NAMES = ("saddr", "daddr", "mntns", "pid", "comm", "lport", "dport", "family", "size", "dir")
@@ -348,10 +348,19 @@ def transport_check(ctx, what, fn):
     rec = {"what": what + ": torch.distributed (nccl = RCCL) vs igx_dist_* (C ABI, RCCL in libigx.so)"}
     ref = fn(D.TorchComm(dist))
     if "igx_comm" not in ctx:
+        # the deadline bounds igx_dist_init too (a rank whose context failed leaves its peers in
+        # ncclCommInitRankConfig until it passes), not only the later collectives
+        old = os.environ.get("IGX_DIST_TIMEOUT_MS")
+        os.environ["IGX_DIST_TIMEOUT_MS"] = str(IGX_CHECK_TIMEOUT_MS)
         try:
             ctx["igx_comm"] = D.IgxComm(dist, timeout_ms=IGX_CHECK_TIMEOUT_MS)
         except Exception as e:   # noqa: BLE001 -- agreed on below
             ctx["igx_comm"], ctx["igx_comm_error"] = None, repr(e)[:300]
+        finally:
+            if old is None:
+                os.environ.pop("IGX_DIST_TIMEOUT_MS", None)
+            else:
+                os.environ["IGX_DIST_TIMEOUT_MS"] = old
         up = torch.tensor([1 if ctx["igx_comm"] is not None else 0], dtype=torch.int32, device=ctx["dev"])
         dist.all_reduce(up, op=dist.ReduceOp.MIN)
         if not int(up.item()) and ctx["igx_comm"] is not None:
@@ -674,7 +683,7 @@ def run_c4(a, ctx):
     tab = E.Table(widths, [], cap)
     # an owner receives about 1/N of the global distinct tuples, but C4's tuple universe is not
     # bounded by one rank's capacity (every rank's slice adds tuples), so its table keeps it
-    own = E.Table(widths, [], cap) if world > 1 else None
+    own = D.owner_table(widths, [], cap) if world > 1 else None
     clk = KernelClock(torch)
     st = {}
 
@@ -719,7 +728,7 @@ def run_c4(a, ctx):
                                 "stream: distinct count + checksum of every (tuple, first index)")
         del keys, valid
     elif a.check:
-        scratch = E.Table(widths, [], cap)
+        scratch = D.owner_table(widths, [], cap)
 
         def c4x(c):
             mine = D.exchange_partitioned(st["part"][0], st["part"][1], c)
@@ -805,8 +814,7 @@ def run_c5(a, ctx):
     tab = E.Table(widths, aggs, cap)
     # C5's key universe is global (C5_CAP bounds it), so an owner holds about 1/N of it
     own_cap = D.owner_capacity(cap, world)
-    own = (E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], own_cap)
-           if world > 1 else None)
+    own = D.owner_table(widths, [8, 8, 8, 8], own_cap) if world > 1 else None
     clk = KernelClock(torch)
     st = {"i": 0}
 
@@ -860,7 +868,7 @@ def run_c5(a, ctx):
                                 "top-20 by [-wbytes] (first + 4 aggregates)")
         del h, keys
     elif a.check:
-        scratch = E.Table(widths, [A.Agg(A.AGG_SUM, 4 + x, A.NO_COL, 8, 0) for x in range(4)], own_cap)
+        scratch = D.owner_table(widths, [8, 8, 8, 8], own_cap)
 
         def c5x(c):
             mine = D.exchange_partitioned(st["part"][0], st["part"][1], c)

@@ -401,8 +401,9 @@ int igx_groupby_destroy(igx_table *t);
  * full update ring, the idle server (bit 16); bit 18, the memory-side atomics: out[8..11] the
  * server wave's updates, of them minima, distinct (value record, opcode) pairs per instruction,
  * distinct (128-B line, opcode) pairs; [12] instructions whose first record continues the
- * previous one's last; [16..19] the same four for the final LDS flush's aggregate updates, [20]
- * its minima.  Counters since the last call. */
+ * previous one's last; [13..15] the distinct (record, opcode) pairs within each 32-, 16- and
+ * 8-lane group of the instruction; [16..19] the same four as [8..11] for the final LDS flush's
+ * aggregate updates, [20] its minima.  Counters since the last call. */
 int igx_groupby_debug_counts(igx_table *t, uint64_t *out32);
 
 /* ---- advise network-policy -------------------------------------------------------------- */

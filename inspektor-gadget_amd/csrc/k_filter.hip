@@ -195,8 +195,11 @@ __global__ __launch_bounds__(TB) void k_filter_compact(const uint64_t *__restric
 
 // k_scan_counts + k_filter_compact in one launch, for up to SF_MAX_TILES tiles: each tile
 // sums the counts of the tiles before it itself (at most SF_MAX_TILES / TB loads per thread),
-// and the last tile writes the survivor count.
-constexpr uint64_t SF_MAX_TILES = 16384;
+// and the last tile writes the survivor count.  That work grows with the square of the tile
+// count; measured per kernel (profiles/r06/filter_scale.txt): 1M rows 7.3 us fused
+// vs 4.6 + 5.6 split, 4M 13.9 vs 9.4 + 5.6, 16M 58.4 vs 26.7 + 5.6 -- so the fused form stops
+// at 4M rows.
+constexpr uint64_t SF_MAX_TILES = 4096;
 __global__ __launch_bounds__(TB) void k_filter_compact_sf(const uint64_t *__restrict__ mask,
                                                           const uint32_t *__restrict__ cnt, uint64_t ntiles,
                                                           uint32_t *__restrict__ out, uint64_t *__restrict__ out_n) {

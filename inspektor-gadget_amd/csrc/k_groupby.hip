@@ -807,6 +807,10 @@ constexpr uint32_t ARING = 512;             // HBM-update ring entries (16 B eac
 // (igx_groupby_finalize then fails with IGX_ENOSPC) instead of hanging the GPU.
 constexpr uint32_t SPIN_LIMIT = 1u << 24;
 constexpr uint32_t WHAT_MIN = 15;           // entry kind: atomicMin on `first`
+// (Round 6 tried padding each lane's run of entries so that no miss's updates straddle an 8-lane
+// group of the server's instruction: the memory-side atomic requests fell by 1M of the 7M that
+// grouping predicted, and the kernels did not get faster -- DESIGN.md §4, "Round 6: the
+// memory-side atomics".  Not kept.)
 // wave roles in a workgroup: a.nl loaders stream rows, the next 15 - a.nl waves (probers)
 // resolve LDS misses against HBM, and the last wave serves the HBM-update ring
 constexpr uint32_t NWAVES = GTB / 64;
@@ -955,7 +959,22 @@ __device__ __forceinline__ void ring_serve(const GbArgs &a, const Ring &r, uint3
             }
         }
         if (DBG && (a.dbg & 262144u)) {
-            atomics_account(a, lane < n, slot, what == WHAT_MIN, lane, 8);
+            const bool live = lane < n;
+            atomics_account(a, live, slot, what == WHAT_MIN, lane, 8);
+            // the same pairs split at 32-, 16- and 8-lane boundaries: which grouping of the
+            // instruction's lanes the memory-side request count follows
+            for (uint32_t g = 0; g < 3; ++g) {
+                const uint32_t sh = 5 - g;
+                uint64_t todo = __ballot(live);
+                uint64_t cnt = 0;
+                while (todo) {
+                    const uint32_t l = (uint32_t)__ffsll((long long)todo) - 1;
+                    const uint32_t s0 = __shfl(slot, (int)l), k0 = __shfl(what == WHAT_MIN ? 1u : 0u, (int)l);
+                    todo &= ~__ballot(live && slot == s0 && (what == WHAT_MIN ? 1u : 0u) == k0 && (lane >> sh) == (l >> sh));
+                    ++cnt;
+                }
+                if (lane == 0) atomicAdd(a.dbg_cnt + 13 + g, (unsigned long long)cnt);
+            }
             const uint32_t first_slot = __shfl(slot, 0), last_slot = __shfl(slot, (int)(n - 1));
             if (lane == 0 && first_slot == prev_last) atomicAdd(a.dbg_cnt + 12, 1ull);
             prev_last = last_slot;
@@ -1486,7 +1505,9 @@ __device__ __forceinline__ void prober(const GbArgs &a, const LdsCache<KW> &c, c
     }
 }
 
-template <class L, bool DBG, int NA>
+// SAMPLE: the same kernel counting the seed sample (seeds_compute), a template instance of its
+// own so that traces and profiles keep its launches apart from the interval's
+template <class L, bool DBG, int NA, bool SAMPLE = false>
 __global__ __launch_bounds__(GTB) void k_groupby(GbArgs a) {
     constexpr int KW = L::KW;
     extern __shared__ uint64_t lds[];
@@ -2328,11 +2349,11 @@ static uint32_t gb_entries_for(uint32_t naggs) {
     return naggs <= 2 ? gb_entries<L, 2>(naggs) : gb_entries<L, AMAX>(naggs);
 }
 
-template <class L, bool DBG, int NA>
+template <class L, bool DBG, int NA, bool SAMPLE = false>
 static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG, NA>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_groupby<L, DBG, NA, SAMPLE>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_TOTAL);
         attr = true;
     }
@@ -2341,7 +2362,7 @@ static void launch_gb_as(igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
     const uint32_t E = gb_entries<L, NA>(a.naggs);
     a.lds_entries = E;
     const size_t lds = E * entry + rings;
-    hipLaunchKernelGGL((k_groupby<L, DBG, NA>), dim3(blocks), dim3(GTB), lds, ctx->stream, a);
+    hipLaunchKernelGGL((k_groupby<L, DBG, NA, SAMPLE>), dim3(blocks), dim3(GTB), lds, ctx->stream, a);
 }
 
 // k_gb_estimate with the cached kernel's geometry (its E and its GHOST filter)
@@ -2673,8 +2694,10 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
 
 // The sample-seeded LDS cache (tools/cache_sim.py: C2 33.7 -> 31.2 % misses, C5 45.4
 // -> 42.6 %, against 30.7 / 42.2 % for an ideal top-E cache).  The first SEED_SAMPLE rows of the
-// interval's first update are counted by key in a scratch table (the cached kernel itself, with
-// one COUNT aggregate), its top-E groups by count are selected on the device (igx_groupby_sort),
+// interval's first update are counted by key in a scratch table (the cached kernel with one COUNT
+// aggregate, as its SAMPLE instance: profiles keep its launches apart; the direct form took
+// 2.7-3.1 ms for these 1.5M rows -- a sample's hot keys queue on one record's atomics), its top-E
+// groups by count are selected on the device (igx_groupby_sort),
 // and k_gb_seeds looks each of them up in the table's current generation.  Every workgroup of the
 // interval's cached updates adopts the found ones before its stream starts.  Hot keys of a
 // stream are stable, so the seeds are recomputed every SEED_EVERY seeded intervals (and after a
@@ -2684,7 +2707,7 @@ constexpr uint64_t SEED_MIN_ROWS = 8u << 20;    // smaller updates: no seeds (IG
 constexpr uint64_t SEED_SAMPLE = 1u << 20;      // sampled rows: max(1M, rows / 64)
 
 template <class L>
-static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
+static int seeds_compute_static(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
     const uint32_t E = gb_entries_for<L>(t->naggs);
     const uint64_t S = std::min<uint64_t>(a.n, std::max<uint64_t>(SEED_SAMPLE, a.n / 64));
     if (t->seed_tab && t->seed_tab->cap < S) {
@@ -2727,6 +2750,7 @@ static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
     b.naggs = 1;
     b.vcount[0] = 1;
     b.hascond[0] = 0;
+    b.valid = a.valid;
     b.krec = st->krec;
     b.vrec = st->vrec;
     b.krec_len = st->krec_len;
@@ -2753,7 +2777,8 @@ static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
     st->fin_since_update = false;
     st->interval_direct = st->interval_part = false;
     st->occb_dirty = true;
-    launch_gb<L>(ctx, b, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((S + GTB - 1) / GTB, (uint64_t)ctx->num_cus)));
+    launch_gb_as<L, false, 2, true>(ctx, b, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((S + GTB - 1) / GTB,
+                                                                                           (uint64_t)ctx->num_cus)));
     IGX_HIP(ctx, hipGetLastError());
     int rc = igx_groupby_finalize_async(st, nullptr);
     if (rc) return rc;
@@ -2768,6 +2793,15 @@ static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
     IGX_HIP(ctx, hipGetLastError());
     t->nseeds = E;
     return IGX_OK;
+}
+
+template <class L>
+static int seeds_compute(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
+    if constexpr (!L::is_static) {
+        return IGX_ENOTSUP;   // static key layouts only (the reference's BPF key structs)
+    } else {
+        return seeds_compute_static<L>(t, ctx, a);
+    }
 }
 
 // one update over layout L in the interval's form
@@ -2800,7 +2834,7 @@ static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
             uint64_t min_rows = SEED_MIN_ROWS;
             if (const char *m = std::getenv("IGX_GB_SEED_MIN")) min_rows = std::strtoull(m, nullptr, 0);
             t->interval_seeded = false;
-            if (t->seed_on && t->gen_planned && !a.dbg && a.n >= min_rows) {
+            if (L::is_static && t->seed_on && t->gen_planned && !a.dbg && a.n >= min_rows) {
                 if (t->seed_left == 0 || !t->nseeds) {
                     if (seeds_compute<L>(t, ctx, a) == IGX_OK) t->seed_left = SEED_EVERY;
                     else t->nseeds = 0;   // no seeds this time (the sample table failed): plain cache

@@ -443,6 +443,88 @@ __global__ __launch_bounds__(TB) void k_compose_u64(ComposeArgs a, uint32_t *__r
     payload[i] = (uint32_t)src;
 }
 
+// k_compose_u64 with k_andor folded in (the tables' top-K): a fixed grid
+// sweeps the rows, CU rows in flight per thread (their slot and value-record loads issued
+// before any is used), composes their words and keeps every word's AND / OR in registers; each
+// block leaves its partials where k_andor would have, so k_andor_final follows unchanged and
+// the composed words are never read back for the reduction.
+constexpr uint32_t CAO_BLOCKS = 2048;   // partials per word (k_andor_final: 32 per lane)
+template <int NK>
+__global__ __launch_bounds__(TB) void k_compose_u64_ao(ComposeArgs a, uint32_t *__restrict__ words,
+                                                       uint32_t *__restrict__ payload, uint32_t *__restrict__ part) {
+    constexpr int KW = 2 * NK + 2;
+    constexpr int CU = 4;
+    __shared__ uint32_t red[2][KW][TB / 64];
+    const uint64_t n = a.d_n ? min(a.n, *a.d_n) : a.n;
+    uint32_t va[KW], vo[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) {
+        va[w] = 0xFFFFFFFFu;
+        vo[w] = 0;
+    }
+    const uint64_t step = (uint64_t)gridDim.x * TB;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * TB + threadIdx.x; i0 < n; i0 += CU * step) {
+        uint64_t src[CU], v[CU][NK], ps[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const uint64_t i = i0 + u * step;
+            src[u] = i < n ? a.rowmap[i] : a.rowmap[i0];
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) v[u][k] = *reinterpret_cast<const uint64_t *>(a.ptr[k] + src[u] * a.rstride[k]);
+            ps[u] = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(a.pos) + src[u] * a.pos_stride);
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const uint64_t i = i0 + u * step;
+            if (i >= n) break;
+            uint32_t wv[KW];
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const uint64_t inv = a.desc[k] ? ~0ull : 0ull;
+                const uint64_t x = (a.kind[k] == IGX_KIND_INT ? v[u][k] ^ (1ull << 63) : v[u][k]) ^ inv;
+                wv[2 * k] = (uint32_t)(x >> 32);
+                wv[2 * k + 1] = (uint32_t)x;
+            }
+            const uint64_t p = a.pos_not ? ~ps[u] : ps[u];
+            wv[2 * NK] = (uint32_t)(p >> 32);
+            wv[2 * NK + 1] = (uint32_t)p;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) {
+                words[(uint64_t)w * a.stride + i] = wv[w];
+                va[w] &= wv[w];
+                vo[w] |= wv[w];
+            }
+            payload[i] = (uint32_t)src[u];
+        }
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int w = 0; w < KW; ++w) {
+        for (int o = 32; o > 0; o >>= 1) {
+            va[w] &= __shfl_xor(va[w], o);
+            vo[w] |= __shfl_xor(vo[w], o);
+        }
+        if (lane == 0) {
+            red[0][w][wave] = va[w];
+            red[1][w][wave] = vo[w];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)KW) {
+        const uint32_t w = threadIdx.x;
+        uint32_t x = 0xFFFFFFFFu, y = 0;
+        for (int j = 0; j < TB / 64; ++j) {
+            x &= red[0][w][j];
+            y |= red[1][w][j];
+        }
+        part[2 * ((uint64_t)w * gridDim.x + blockIdx.x)] = x;
+        part[2 * ((uint64_t)w * gridDim.x + blockIdx.x) + 1] = y;
+    }
+}
+
 // per-word AND / OR over all rows -> part[(w * gridDim.x + block) * 2 + {0: and, 1: or}].
 // 16-byte loads, four in flight per lane; partials, not atomics: the words' results share
 // one line, and same-line atomics from every workgroup serialise at the memory side.
@@ -1735,7 +1817,8 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
     const size_t hist_b = igx_align((size_t)256 * nblocks * 4, 256) +
                           igx_align(((size_t)256 * nblocks + SCAN_CHUNK - 1) / SCAN_CHUNK * 4, 256);
     constexpr uint32_t ANDOR_BLOCKS = 256;
-    const size_t res_b = igx_align((size_t)KW * 8 + 16, 256) + igx_align((size_t)KW * ANDOR_BLOCKS * 8, 256);
+    const size_t res_b = igx_align((size_t)KW * 8 + 16, 256) +
+                         igx_align((size_t)KW * std::max<uint32_t>(ANDOR_BLOCKS, CAO_BLOCKS) * 8, 256);
     const bool use_sel = limit && limit <= SEL_SMALL_K && nrows > 2ull * limit;
     // Full sorts without float keys may plan their passes on the device (k_lsd_*: no host read at
     // all) with IGX_SORT_DEVPLAN=1.  Measured on C1 (1M rows, 16 live digits) they are slower
@@ -1870,7 +1953,17 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                     return igx_fail(ctx, IGX_EIO, "sort: k_dict_rank launch: %s", hipGetErrorString(le));
             }
         }
-        if (u64_shape) {
+        uint32_t *apart = res + igx_align((size_t)KW * 2 + 4, 64);
+        uint32_t fused_ao = 0;   // k_compose_u64_ao's grid: it left the AND / OR partials
+        if (u64_shape && !use_lsd) {
+            fused_ao = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(CAO_BLOCKS, (nrows + 4 * TB - 1) / (4 * TB)));
+            switch (nkeys) {
+            case 1: hipLaunchKernelGGL(k_compose_u64_ao<1>, dim3(fused_ao), dim3(TB), 0, ctx->stream, ca, W[0], P[0], apart); break;
+            case 2: hipLaunchKernelGGL(k_compose_u64_ao<2>, dim3(fused_ao), dim3(TB), 0, ctx->stream, ca, W[0], P[0], apart); break;
+            case 3: hipLaunchKernelGGL(k_compose_u64_ao<3>, dim3(fused_ao), dim3(TB), 0, ctx->stream, ca, W[0], P[0], apart); break;
+            default: hipLaunchKernelGGL(k_compose_u64_ao<4>, dim3(fused_ao), dim3(TB), 0, ctx->stream, ca, W[0], P[0], apart); break;
+            }
+        } else if (u64_shape) {
             switch (nkeys) {
             case 1: hipLaunchKernelGGL(k_compose_u64<1>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
             case 2: hipLaunchKernelGGL(k_compose_u64<2>, dim3(cblocks), dim3(TB), 0, ctx->stream, ca, W[0], P[0]); break;
@@ -1916,9 +2009,12 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             IGX_HIP(ctx, hipGetLastError());
             return IGX_OK;
         }
-        ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
-        uint32_t *apart = res + igx_align((size_t)KW * 2 + 4, 64);
-        hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
+        if (fused_ao) {
+            ablocks = fused_ao;
+        } else {
+            ablocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ANDOR_BLOCKS, nrows / (4 * TB)));
+            hipLaunchKernelGGL(k_andor, dim3(ablocks, KW), dim3(TB), 0, ctx->stream, W[0], nrows, stride, apart, d_nrows);
+        }
         if (use_sel && !any_float && rowmap) {
             // top-K of a table's groups without host round trips (SelState on the device): no float
             // key, so no NaN check; the first differing bit is found on the device; the position

@@ -75,7 +75,8 @@ def main():
                 if v & 262144:
                     res.setdefault("atomics", []).append(
                         {"server_updates": cnt[8], "server_minima": cnt[9], "server_record_requests": cnt[10],
-                         "server_line_requests": cnt[11], "server_straddles": cnt[12], "flush_updates": cnt[16],
+                         "server_line_requests": cnt[11], "server_straddles": cnt[12],
+                         "server_pairs_by_32_16_8_lanes": [cnt[13], cnt[14], cnt[15]], "flush_updates": cnt[16],
                          "flush_record_requests": cnt[18], "flush_minima": cnt[20],
                          "claims": tab.info()["claims"]})
     os.environ.pop("IGX_GB_DEBUG", None)

@@ -32,7 +32,7 @@ def main():
     p.add_argument("--ranks", type=int, default=8)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--configs", default="c5,c4")
-    p.add_argument("--merge-mode", default="auto", choices=("auto", "cached", "direct", "part"),
+    p.add_argument("--merge-mode", default="cached", choices=("auto", "cached", "direct", "part"),
                    help="the owner table's group-by form (igx_groupby_set_mode)")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06", "emulated_rank8.json"))
     a = p.parse_args()

@@ -1,6 +1,7 @@
 # the memory-side atomics of the cached group-by, counted two ways on the
 # same launches -- the debug kernel's per-kind counters (IGX_GB_DEBUG bit 18, libigx_dbg.so
-# built with -DIGX_GB_DEBUG_FILE) and rocprofv3's TCC_EA0_ATOMIC -- for C5 (top file) and C2.
+# built with -DIGX_GB_DEBUG_FILE: make -C inspektor-gadget_amd/csrc OUT=../libigx_dbg.so OBJDIR=../.build_dbg
+# EXTRA=-DIGX_GB_DEBUG_FILE) and rocprofv3's TCC_EA0_ATOMIC -- for C5 (top file) and C2.
 # Three launches per layout over one batch: the first starts a generation (claims), the next two
 # keep its keys.   bash tools/gpu/r06_atomics.sh -> gpurun_out/atom/
 set -o pipefail

@@ -17,7 +17,7 @@ import json
 import os
 
 
-def _values(d, counter, kernel):
+def _values(d, counter, kernel, exclude=()):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -25,7 +25,8 @@ def _values(d, counter, kernel):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row["Counter_Name"] == counter and kernel in row["Kernel_Name"]:
+                name = row["Kernel_Name"]
+                if row["Counter_Name"] == counter and kernel in name and not any(x in name for x in exclude):
                     vals.append(float(row["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for kernel {kernel!r} in {d}")
@@ -42,11 +43,13 @@ def main():
                         "and divide by the launches of this one")
     p.add_argument("--extra", action="append", default=[],
                    help="another kernel of the same step whose per-launch traffic is added (e.g. k_np_mark)")
+    p.add_argument("--exclude", action="append", default=[],
+                   help="skip kernels whose name holds this (e.g. the group-by's SAMPLE instance, ', true>')")
     p.add_argument("--config", required=True)
     p.add_argument("--out", required=True)
     a = p.parse_args()
-    f = _values(a.fetch, "FETCH_SIZE", a.kernel)
-    w = _values(a.write, "WRITE_SIZE", a.kernel)
+    f = _values(a.fetch, "FETCH_SIZE", a.kernel, a.exclude)
+    w = _values(a.write, "WRITE_SIZE", a.kernel, a.exclude)
     nf, nw = len(f), len(w)
     if a.anchor:
         nf = len(_values(a.fetch, "FETCH_SIZE", a.anchor))
@@ -60,7 +63,7 @@ def main():
     out = {"kernel": a.kernel, "extra": a.extra, "config": json.loads(a.config),
            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
            "traffic_bytes_per_launch": fetch_b + write_b, "launches": [nf, nw],
-           "anchor": a.anchor,
+           "anchor": a.anchor, "exclude": a.exclude,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> bytes"}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
