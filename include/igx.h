@@ -395,6 +395,10 @@ int igx_groupby_set_mode(igx_table *t, uint32_t mode);
  * igx_groupby_finalize.  Asynchronous. */
 int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t nkeys, uint32_t k,
                      uint32_t *out_slots);
+/* Diagnostics (synchronous): out2[0] = top-Ks of this table answered by the hinted path (the
+ * slots of the same sort's last top-K bound the k-th key; only the groups at or below the bound
+ * are ranked), out2[1] = top-Ks answered by the full selection.  Both give the same slots. */
+int igx_groupby_topk_counts(igx_table *t, uint64_t *out2);
 int igx_groupby_destroy(igx_table *t);
 /* Diagnostics only (IGX_GB_DEBUG env), 32 words: out[0..1] LDS-cache hits / misses (bit 3);
  * out[4..7] sleep counts of loaders on a full miss ring, probers on an empty one, probers on a

@@ -153,6 +153,7 @@ SIGNATURES = [
     ("igx_groupby_set_mode", _I, [_VP, _U32]),
     ("igx_groupby_destroy", _I, [_VP]),
     ("igx_groupby_debug_counts", _I, [_VP, _VP]),
+    ("igx_groupby_topk_counts", _I, [_VP, _VP]),
     ("igx_np_mark", _I, [_VP, _VP, _VP, _VP, _VP, _U64, _VP]),
     ("igx_hist_log2", _I, [_VP, _VP, _VP, _VP, _U64, C.POINTER(_U32), _U32, _U32, _U64, _U32,
                            _VP]),

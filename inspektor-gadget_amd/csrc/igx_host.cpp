@@ -586,7 +586,7 @@ extern "C" int igx_sort_prepare(const igx_schema_col *cols, uint32_t ncols, cons
 static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                        uint64_t nrows, const uint64_t *pos, const uint8_t *valid, uint32_t *out, uint32_t limit,
                        const uint32_t *rowmap, uint32_t pos_stride = 8, uint32_t direct_mask = 0,
-                       const uint64_t *d_nrows = nullptr) {
+                       const uint64_t *d_nrows = nullptr, TopkHint *hint = nullptr) {
     if (!ctx) return IGX_EINVAL;
     if (nrows == 0) return IGX_OK;                          // sort.go:36-38
     if (!out) return igx_fail(ctx, IGX_EINVAL, "sort: null output");
@@ -629,14 +629,15 @@ static int sort_common(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *st
         return launch_sort_perm(ctx, nullptr, 0, nrows, nullptr, false, nullptr, out, limit, rowmap);
     }
     return launch_sort_perm(ctx, plan.data(), (uint32_t)plan.size(), nrows, pos, parity != 0, valid, out, limit,
-                            rowmap, pos_stride, go.data(), (uint32_t)go.size(), d_nrows);
+                            rowmap, pos_stride, go.data(), (uint32_t)go.size(), d_nrows, hint);
 }
 
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
-                     uint32_t limit, uint32_t *out, uint32_t direct_mask, const uint64_t *d_nrows) {
+                     uint32_t limit, uint32_t *out, uint32_t direct_mask, const uint64_t *d_nrows,
+                     TopkHint *hint) {
     return sort_common(ctx, keys, strides, nkeys, nrows, pos, nullptr, out, limit, rowmap, pos_stride, direct_mask,
-                       d_nrows);
+                       d_nrows, hint);
 }
 
 extern "C" int igx_ip_text(igx_ctx *ctx, const uint8_t *addr, uint32_t addr_stride, const uint8_t *family,

@@ -108,18 +108,32 @@ struct GoSortKey {
 // case returns IGX_ENOTSUP).  d_nrows (device, nullable): the row count lives on the device and
 // nrows is only its upper bound -- top-K without a float key or nil mask only (the device
 // selection); out_perm entries past the count are 0xFFFFFFFF.
+// A table's top-K hint (k_sort.hip, the device selection over a table's groups): the slots
+// of its last top-K.  The k smallest composed keys of ALL groups are <= the k-th smallest of
+// ANY k groups, so the groups at or below that bound hold the top-K whatever the hints are:
+// hints only decide how tight the bound is (how few rows are ranked), never the result.
+constexpr uint32_t TK_MAXK = 1024;
+constexpr size_t TK_STATE_BYTES = 64 + 2048 * 4;   // counters + bound, then the candidates
+struct TopkHint {
+    uint32_t *slots;       // device, TK_MAXK words: read, then rewritten with this call's top-K
+    uint32_t nh;           // slots held (0: none yet); the call sets it to its k
+    const uint32_t *occ;   // the interval's occupancy bitmap: a hint counts iff its slot is a group
+    uint64_t nslots;
+    uint32_t *state;       // device, TK_STATE_BYTES
+};
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap,
                      uint32_t pos_stride = 8, const GoSortKey *gokeys = nullptr, uint32_t ngokeys = 0,
-                     const uint64_t *d_nrows = nullptr);
+                     const uint64_t *d_nrows = nullptr, TopkHint *hint = nullptr);
 // data (device, n rows in the pre-sort order) sorted in place by Go 1.19 SliceStable, pass by pass
 int launch_go_stable(igx_ctx *ctx, const GoSortKey *keys, uint32_t nkeys, uint64_t nrows, const uint8_t *valid,
                      uint32_t *data);
 // closed-form planning + launch (igx_host.cpp); strides per key (nullable = widths)
 int sort_common_rows(igx_ctx *ctx, const igx_sortkey *keys, const uint32_t *strides, uint32_t nkeys,
                      uint64_t nrows, const uint32_t *rowmap, const uint64_t *pos, uint32_t pos_stride,
-                     uint32_t limit, uint32_t *out, uint32_t direct_mask = 0, const uint64_t *d_nrows = nullptr);
+                     uint32_t limit, uint32_t *out, uint32_t direct_mask = 0, const uint64_t *d_nrows = nullptr,
+                     TopkHint *hint = nullptr);
 
 int launch_hist_log2(igx_ctx *ctx, const uint32_t *dev, const uint32_t *cont,
                      const int64_t *delta, uint64_t nrows, const uint32_t *devs, uint32_t ndev,

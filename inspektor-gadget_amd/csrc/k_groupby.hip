@@ -2119,6 +2119,14 @@ struct igx_table {
     bool interval_probe = false;   // AUTO: the last partitioned interval of a run (k_gb_estimate)
     uint64_t probe_rows = 0;       // ... the rows its estimator replayed
     unsigned long long *dbg_cnt = nullptr;
+    // the last top-K's slots per sort (keys + k): the next same top-K's hint (TopkHint)
+    struct TkHint {
+        uint64_t sig = 0, used = 0;
+        uint32_t *slots = nullptr;
+        uint32_t nh = 0;
+    } tk[4];
+    uint32_t *tk_state = nullptr;
+    uint64_t tk_clock = 0;
     uint8_t *text[32] = {};      // IP text of the groups, per IGX_TSRC_IPTEXT sort key
     uint64_t text_rows[32] = {};
 };
@@ -2320,6 +2328,8 @@ extern "C" int igx_groupby_destroy(igx_table *t) {
     (void)hipFree(t->p_recs);
     (void)hipFree(t->p_cnt);
     (void)hipFree(t->p_mask);
+    for (auto &h : t->tk) (void)hipFree(h.slots);
+    (void)hipFree(t->tk_state);
     for (auto *p : t->text) (void)hipFree(p);
     if (t->fin_host) (void)hipHostFree(t->fin_host);
     delete t;
@@ -3431,8 +3441,66 @@ extern "C" int igx_groupby_sort(igx_table *t, const igx_tsortkey *keys, uint32_t
             return igx_fail(ctx, IGX_EINVAL, "groupby_sort: bad source");
         }
     }
-    return sort_common_rows(ctx, sk, strides, nkeys, nrows, t->groups, t->vrec, t->vrec_len, k, out_slots, direct,
-                            d_count);
+    // the hint of the table's repeated top-K (k_sort.hip k_tk_*): any slots give an exact answer,
+    // the last top-K's give a tight bound
+    TopkHint hint{};
+    igx_table::TkHint *th = nullptr;
+    if (k > 0 && k <= TK_MAXK) {
+        uint64_t sig = 0xcbf29ce484222325ull;   // FNV-1a over the sort's description
+        auto mix = [&sig](uint64_t v) {
+            for (int b = 0; b < 8; ++b) sig = (sig ^ ((v >> (8 * b)) & 0xFF)) * 0x100000001b3ull;
+        };
+        mix(k);
+        mix(nkeys);
+        for (uint32_t i = 0; i < nkeys; ++i) {
+            const igx_tsortkey &q = keys[i];
+            mix(q.src);
+            mix(q.index);
+            mix(q.desc);
+            mix(q.offset);
+            mix(q.width);
+            mix(q.kind);
+        }
+        sig |= 1;
+        for (auto &h : t->tk)
+            if (h.sig == sig) th = &h;
+        if (!th) {   // a new sort: the least recently used entry
+            th = &t->tk[0];
+            for (auto &h : t->tk)
+                if (h.used < th->used) th = &h;
+            th->sig = sig;
+            th->nh = 0;
+        }
+        th->used = ++t->tk_clock;
+        if (!th->slots) IGX_HIP(ctx, hipMalloc(&th->slots, TK_MAXK * 4));
+        if (!t->tk_state) {
+            IGX_HIP(ctx, hipMalloc(&t->tk_state, TK_STATE_BYTES));
+            IGX_HIP(ctx, hipMemsetAsync(t->tk_state, 0, TK_STATE_BYTES, ctx->stream));
+        }
+        hint.slots = th->slots;
+        hint.nh = th->nh;
+        hint.occ = t->occ;
+        hint.nslots = t->nslots;
+        hint.state = t->tk_state;
+    }
+    const int rc = sort_common_rows(ctx, sk, strides, nkeys, nrows, t->groups, t->vrec, t->vrec_len, k, out_slots,
+                                    direct, d_count, th ? &hint : nullptr);
+    if (th) th->nh = rc == IGX_OK ? hint.nh : 0;
+    return rc;
+}
+
+// Diagnostics: how the table's top-Ks were answered so far (synchronous).
+extern "C" int igx_groupby_topk_counts(igx_table *t, uint64_t *out2) {
+    if (!t || !out2) return IGX_EINVAL;
+    igx_ctx *ctx = t->ctx;
+    out2[0] = out2[1] = 0;
+    if (!t->tk_state) return IGX_OK;
+    uint32_t w[2];
+    IGX_HIP(ctx, hipMemcpyAsync(w, t->tk_state + 14, 8, hipMemcpyDeviceToHost, ctx->stream));
+    IGX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    out2[0] = w[0];
+    out2[1] = w[1];
+    return IGX_OK;
 }
 
 // Diagnostics only: LDS-cache hit / miss counters collected when IGX_GB_DEBUG has bit 3.

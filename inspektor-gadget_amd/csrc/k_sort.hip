@@ -351,6 +351,7 @@ struct ComposeArgs {
     uint32_t *nan_seen;   // set to 1 when a float key of a non-nil row is NaN (k_andor_final
                           // moves it into res and clears it: the word is the context's, zero
                           // between sorts)
+    const uint32_t *skip; // nullable: nonzero on the device when a hinted top-K already answered
 };
 
 __global__ __launch_bounds__(TB) void k_compose(ComposeArgs a, uint32_t *__restrict__ words,
@@ -455,6 +456,7 @@ __global__ __launch_bounds__(TB) void k_compose_u64_ao(ComposeArgs a, uint32_t *
     constexpr int KW = 2 * NK + 2;
     constexpr int CU = 4;
     __shared__ uint32_t red[2][KW][TB / 64];
+    if (a.skip && *a.skip) return;
     const uint64_t n = a.d_n ? min(a.n, *a.d_n) : a.n;
     uint32_t va[KW], vo[KW];
 #pragma unroll
@@ -582,6 +584,7 @@ __global__ __launch_bounds__(TB) void k_andor(const uint32_t *__restrict__ words
 struct SelState;
 __device__ void sel_state_init(const uint32_t *res, uint32_t nw, uint64_t n, uint32_t k, SelState *st,
                                const uint64_t *d_n);
+__device__ void sel_state_skip(SelState *st, uint32_t k);
 
 // res[2w], res[2w + 1] = AND / OR of word w over k_andor's nb partials (one wave per word),
 // res[2 kw] = the NaN flag, which is cleared for the next sort, res[2 kw + 1] = a void string
@@ -591,8 +594,13 @@ __global__ __launch_bounds__(1024) void k_andor_final(const uint32_t *__restrict
                                                       uint32_t *__restrict__ res, uint32_t *__restrict__ nan_seen,
                                                       SelState *st, uint64_t n, uint32_t k,
                                                       const uint64_t *__restrict__ d_n, uint32_t *__restrict__ hist,
-                                                      const uint32_t *__restrict__ dctl = nullptr, uint32_t ndict = 0) {
+                                                      const uint32_t *__restrict__ dctl = nullptr, uint32_t ndict = 0,
+                                                      const uint32_t *skip = nullptr) {
     __shared__ uint32_t r[2 * MAXW];
+    if (skip && *skip) {   // a hinted top-K answered: the selection passes find nothing to do
+        if (st && threadIdx.x == 0) sel_state_skip(st, k);
+        return;
+    }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t w = wave; w < KW; w += 1024 / 64) {
         uint32_t va = 0xFFFFFFFFu, vo = 0;
@@ -1331,6 +1339,15 @@ __device__ void sel_state_init(const uint32_t *res, uint32_t nw, uint64_t n, uin
     st->err = 0;
 }
 
+// no rows: the selection passes return at once
+__device__ void sel_state_skip(SelState *st, uint32_t k) {
+    st->n = 0;
+    st->krem = k;
+    st->nbits = 0;
+    st->b = 0;
+    st->acc_cnt = st->out_cnt = st->err = 0;
+}
+
 __global__ __launch_bounds__(TB) void k_sel_hist_d(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                    const SelState *__restrict__ st, uint32_t *__restrict__ hist) {
     __shared__ uint32_t h[SEL_BINS];
@@ -1475,9 +1492,10 @@ __global__ __launch_bounds__(TB) void k_sel_split_d(const uint32_t *__restrict__
 __global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                      SelState *st, uint32_t *__restrict__ acc, uint32_t *cnd0,
                                                      uint32_t *cnd1, uint32_t k, const uint32_t *__restrict__ payload,
-                                                     uint32_t *__restrict__ out) {
+                                                     uint32_t *__restrict__ out, const uint32_t *skip = nullptr) {
     __shared__ uint32_t h[SEL_BINS];
     __shared__ uint32_t tmp[20], cnt[2];
+    if (skip && *skip) return;
     uint32_t n = st->n, krem = st->krem, bitpos = st->bitpos, nbits = st->nbits, nacc = 0;
     const uint32_t *cand = nullptr;   // nullptr: rows 0..n-1
     uint32_t *nxt = cnd0;
@@ -1552,8 +1570,9 @@ __global__ __launch_bounds__(1024) void k_sel_finish(const uint32_t *__restrict_
 __global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W, uint64_t stride, uint32_t nw,
                                                  const uint32_t *__restrict__ acc, uint32_t k,
                                                  const uint32_t *__restrict__ payload, uint32_t *__restrict__ out,
-                                                 const SelState *__restrict__ st) {
+                                                 const SelState *__restrict__ st, const uint32_t *skip = nullptr) {
     __shared__ uint32_t red[TB / 64];
+    if (skip && *skip) return;
     const uint32_t r = blockIdx.x;
     if (st) {   // the row count was on the device: fewer rows than k leave the tail unset
         k = min(k, st->n);
@@ -1581,6 +1600,186 @@ __global__ __launch_bounds__(TB) void k_sel_rank(const uint32_t *__restrict__ W,
         for (int w = 0; w < TB / 64; ++w) t += red[w];
         out[t] = payload[me];
     }
+}
+
+// ---- the tables' repeated top-K, bounded by a hint ------------------------------------------
+// A table's top-K is asked for again every interval, and the groups it returned last time are
+// mostly near the top again.  Their keys this interval bound the k-th key (TopkHint,
+// igx_internal.h): k_tk_bound finds the k-th smallest composed key among the hinted slots that
+// are groups of this interval, k_tk_filter reads one key word per group and keeps the groups at
+// or below it (usually a few dozen), k_tk_rank ranks them in one workgroup.  No composed word
+// arrays and no selection passes: the tail reads each group's sort key once.  When the bound
+// leaves more candidates than one workgroup ranks (or fewer than k hints are groups), `done`
+// stays 0 and the full selection runs after it as before; its kernels read `done` and return
+// at once when the hinted path answered.
+// state: words [0] candidates, [1] done, [2] no bound; the bound (NK + 1 u64) from byte 16;
+// [14] / [15] the top-Ks the hinted / the full path answered (igx_groupby_topk_counts); the
+// candidates from word 16.
+template <int NK>
+constexpr uint32_t tk_cc() { return NK <= 2 ? 2048u : 1024u; }   // candidates k_tk_rank holds in LDS
+static_assert(64 + 2048 * 4 <= TK_STATE_BYTES, "state holds the candidates");
+
+template <int NK>
+__device__ __forceinline__ void tk_tuple(const ComposeArgs &a, uint64_t src, uint64_t (&t)[NK + 1]) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) t[k] = *reinterpret_cast<const uint64_t *>(a.ptr[k] + src * a.rstride[k]);
+    const uint64_t p = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(a.pos) + src * a.pos_stride);
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+        t[k] = (a.kind[k] == IGX_KIND_INT ? t[k] ^ (1ull << 63) : t[k]) ^ (a.desc[k] ? ~0ull : 0ull);
+    t[NK] = a.pos_not ? ~p : p;
+}
+
+// -1 / 0 / 1: x before / equal to / after y in the composed order
+template <int NK>
+__device__ __forceinline__ int tk_cmp(const uint64_t *x, const uint64_t *y) {
+#pragma unroll
+    for (int k = 0; k <= NK; ++k)
+        if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+    return 0;
+}
+
+template <int NK>
+__global__ __launch_bounds__(1024) void k_tk_bound(ComposeArgs a, const uint32_t *__restrict__ hints, uint32_t nh,
+                                                   const uint32_t *__restrict__ occ, uint64_t nslots, uint32_t k,
+                                                   uint32_t *__restrict__ st) {
+    __shared__ uint64_t tup[TK_MAXK][NK + 1];
+    __shared__ uint32_t ok[TK_MAXK];
+    const uint32_t h = threadIdx.x;
+    bool v = false;
+    if (h < nh) {
+        const uint32_t s = hints[h];
+        v = s < nslots && ((occ[s >> 5] >> (s & 31)) & 1u);
+        if (v) {
+            uint64_t t[NK + 1];
+            tk_tuple<NK>(a, s, t);
+#pragma unroll
+            for (int w = 0; w <= NK; ++w) tup[h][w] = t[w];
+        }
+    }
+    ok[h] = v ? 1u : 0u;
+    const uint32_t nvalid = (uint32_t)__syncthreads_count(v);
+    if (nvalid < k) {   // no bound: the full selection answers
+        if (h == 0) {
+            st[0] = 0;
+            st[1] = 0;
+            st[2] = 1;
+        }
+        return;
+    }
+    if (v) {
+        uint32_t less = 0, eq = 0;
+        for (uint32_t j = 0; j < nh; ++j) {
+            if (!ok[j]) continue;
+            const int c = tk_cmp<NK>(tup[j], tup[h]);
+            less += c < 0;
+            eq += c == 0;
+        }
+        if (less <= k - 1 && less + eq > k - 1) {   // the k-th smallest (equal hints write the same)
+            uint64_t *b = reinterpret_cast<uint64_t *>(st + 4);
+#pragma unroll
+            for (int w = 0; w <= NK; ++w) b[w] = tup[h][w];
+        }
+    }
+    if (h == 0) {
+        st[0] = 0;
+        st[1] = 0;
+        st[2] = 0;
+    }
+}
+
+// the groups whose composed key is at or below the bound -> candidates (slots); past tk_cc they
+// are only counted.  One key word per group decides unless it equals the bound's.
+template <int NK>
+__global__ __launch_bounds__(TB) void k_tk_filter(ComposeArgs a, uint32_t *__restrict__ st) {
+    constexpr int CU = 4;
+    if (st[2]) return;
+    const uint64_t *bp = reinterpret_cast<const uint64_t *>(st + 4);
+    const uint64_t b0 = bp[0];
+    uint32_t *cand = st + 16;
+    const uint64_t n = a.d_n ? min(a.n, *a.d_n) : a.n;
+    const uint64_t inv0 = a.desc[0] ? ~0ull : 0ull;
+    const uint64_t sg0 = a.kind[0] == IGX_KIND_INT ? 1ull << 63 : 0ull;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)gridDim.x * TB;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * TB + threadIdx.x; i0 - lane < n; i0 += CU * step) {
+        uint64_t src[CU], x[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const uint64_t i = i0 + u * step;
+            src[u] = a.rowmap[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u) x[u] = *reinterpret_cast<const uint64_t *>(a.ptr[0] + src[u] * a.rstride[0]);
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const uint64_t i = i0 + u * step;
+            const uint64_t c0 = (x[u] ^ sg0) ^ inv0;
+            bool take = false;
+            if (i < n) {
+                if (c0 < b0) {
+                    take = true;
+                } else if (c0 == b0) {
+                    uint64_t t[NK + 1];
+                    tk_tuple<NK>(a, src[u], t);
+                    take = tk_cmp<NK>(t, bp) <= 0;
+                }
+            }
+            const uint64_t m = __ballot(take);
+            if (m) {
+                uint32_t base = 0;
+                if (lane == (uint32_t)__ffsll((long long)m) - 1) base = atomicAdd(&st[0], (uint32_t)__popcll(m));
+                base = __shfl(base, __ffsll((long long)m) - 1);
+                const uint32_t r = base + (uint32_t)__popcll(m & lanemask_lt());
+                if (take && r < tk_cc<NK>()) cand[r] = (uint32_t)src[u];
+            }
+        }
+    }
+}
+
+// rank the candidates (full composed keys, in LDS) -> out[0 .. k) and the next call's hints;
+// done = 1.  More candidates than fit, or none bound: done stays 0.
+template <int NK>
+__global__ __launch_bounds__(1024) void k_tk_rank(ComposeArgs a, uint32_t *__restrict__ st, uint32_t k,
+                                                  uint32_t *__restrict__ out, uint32_t *__restrict__ hints) {
+    constexpr uint32_t CC = tk_cc<NK>();
+    __shared__ uint64_t tup[CC][NK + 1];
+    __shared__ uint32_t slot[CC];
+    const uint32_t m = st[0];
+    if (st[2] || m > CC || m < k) return;
+    const uint32_t *cand = st + 16;
+    for (uint32_t j = threadIdx.x; j < m; j += 1024) {
+        const uint32_t s = cand[j];
+        slot[j] = s;
+        uint64_t t[NK + 1];
+        tk_tuple<NK>(a, s, t);
+#pragma unroll
+        for (int w = 0; w <= NK; ++w) tup[j][w] = t[w];
+    }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < m; r += 1024) {
+        uint32_t less = 0;
+        for (uint32_t j = 0; j < m; ++j) less += tk_cmp<NK>(tup[j], tup[r]) < 0;
+        if (less < k) {
+            out[less] = slot[r];
+            hints[less] = slot[r];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st[1] = 1;
+        st[14] += 1;
+    }
+}
+
+// the full selection answered (done == 0, or no hinted path ran: done null): its top-K become
+// the next call's hints
+__global__ __launch_bounds__(1024) void k_tk_save(const uint32_t *__restrict__ out, uint32_t k,
+                                                  uint32_t *__restrict__ hints, const uint32_t *done,
+                                                  uint32_t *__restrict__ st) {
+    if (done && *done) return;
+    for (uint32_t r = threadIdx.x; r < k; r += 1024) hints[r] = out[r];
+    if (threadIdx.x == 0) st[15] += 1;
 }
 
 // ---- IP address text (gadgets.IPStringFromBytes, pkg/gadgets/helpers.go:111-120) ----------
@@ -1770,7 +1969,7 @@ static int sort_exact_go(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, 
 int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint64_t nrows,
                      const uint64_t *pos, bool pos_not, const uint8_t *valid,
                      uint32_t *out_perm, uint32_t limit, const uint32_t *rowmap, uint32_t pos_stride,
-                     const GoSortKey *gokeys, uint32_t ngokeys, const uint64_t *d_nrows) {
+                     const GoSortKey *gokeys, uint32_t ngokeys, const uint64_t *d_nrows, TopkHint *hint) {
     if (nrows == 0) return IGX_OK;
     if (nrows >= (1ull << 32)) return igx_fail(ctx, IGX_EINVAL, "sort: too many rows");
     if (nkeys > NSK) return igx_fail(ctx, IGX_ENOTSUP, "sort: more than %d keys", NSK);
@@ -1911,6 +2110,37 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                     keys[k].words == 2 && !keys[k].direct;
     uint32_t *hres = nullptr;
     uint32_t ablocks = 0;
+    // A table's top-K with a hint (k_tk_*): the hinted path runs first and the full selection
+    // after it only does work when the hinted path could not answer.
+    const char *tk_e = std::getenv("IGX_TOPK_HINT");   // A/B knob: 0 = always the full selection
+    const bool tk_env = !(tk_e && std::strcmp(tk_e, "0") == 0);
+    const char *tk_m = std::getenv("IGX_TOPK_HINT_MIN");   // rows below which the full selection is cheap anyway
+    const uint64_t tk_min = tk_m ? std::strtoull(tk_m, nullptr, 0) : 65536ull;
+    const bool tk_on = hint && tk_env && u64_shape && use_sel && !use_lsd && !any_float && rowmap && !valid &&
+                       ndict == 0 && limit <= TK_MAXK && nrows >= tk_min;
+    const uint32_t *tk_done = nullptr;
+    if (tk_on && hint->nh) {
+        uint32_t *st = hint->state;
+        const uint32_t nh = std::min<uint32_t>(hint->nh, TK_MAXK);
+        const uint32_t fb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(CAO_BLOCKS, (nrows + 4 * TB - 1) / (4 * TB)));
+        switch (nkeys) {
+#define IGX_TK_LAUNCH(NK)                                                                                              \
+    case NK:                                                                                                           \
+        hipLaunchKernelGGL(k_tk_bound<NK>, dim3(1), dim3(TK_MAXK), 0, ctx->stream, ca, hint->slots, nh, hint->occ,     \
+                           hint->nslots, limit, st);                                                                   \
+        hipLaunchKernelGGL(k_tk_filter<NK>, dim3(fb), dim3(TB), 0, ctx->stream, ca, st);                               \
+        hipLaunchKernelGGL(k_tk_rank<NK>, dim3(1), dim3(1024), 0, ctx->stream, ca, st, limit, out_perm, hint->slots);  \
+        break;
+            IGX_TK_LAUNCH(1)
+            IGX_TK_LAUNCH(2)
+            IGX_TK_LAUNCH(3)
+            IGX_TK_LAUNCH(4)
+#undef IGX_TK_LAUNCH
+        }
+        IGX_HIP(ctx, hipGetLastError());
+        tk_done = st + 1;
+    }
+    ca.skip = tk_done;
     // Compose, reduce, read back.  With dictionaries the first attempt composes the ranks; a
     // void dictionary (more distinct values than it holds) is seen in the read-back, and the
     // second attempt composes the raw bytes.
@@ -2027,7 +2257,7 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
             SelState *stp = reinterpret_cast<SelState *>(cnd[1] + stride);
             uint32_t *dh = reinterpret_cast<uint32_t *>(stp) + 64;   // SEL_BINS
             hipLaunchKernelGGL(k_andor_final, dim3(1), dim3(1024), 0, ctx->stream, apart, ablocks, KW, res,
-                               ctx->nan_word, stp, nrows, limit, d_nrows, dh, nullptr, 0u);
+                               ctx->nan_word, stp, nrows, limit, d_nrows, dh, nullptr, 0u, tk_done);
             // about 16 rows per thread: each workgroup adds its nonzero bins to the global
             // histogram, and a skewed table's low bins take one same-address atomic per workgroup
             const uint32_t hb = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(64, nrows / (16 * TB)));
@@ -2036,10 +2266,15 @@ int launch_sort_perm(igx_ctx *ctx, const SortPlanKey *keys, uint32_t nkeys, uint
                                W[0], stride, KW, stp, dh, acc, cnd[0]);
             const bool fused = limit <= 1024 && (uint64_t)limit * KW <= SEL_BINS;   // the k rows' words fit its LDS
             hipLaunchKernelGGL(k_sel_finish, dim3(1), dim3(1024), 0, ctx->stream, W[0], stride, KW, stp, acc, cnd[0],
-                               cnd[1], limit, P[0], fused ? out_perm : nullptr);
+                               cnd[1], limit, P[0], fused ? out_perm : nullptr, tk_done);
             if (!fused)
                 hipLaunchKernelGGL(k_sel_rank, dim3(limit), dim3(TB), 0, ctx->stream, W[0], stride, KW, acc, limit, P[0],
-                                   out_perm, stp);
+                                   out_perm, stp, tk_done);
+            if (tk_on) {   // the full selection's answer (if it ran) becomes the next call's hints
+                hipLaunchKernelGGL(k_tk_save, dim3(1), dim3(1024), 0, ctx->stream, out_perm, limit, hint->slots, tk_done,
+                                   hint->state);
+                hint->nh = limit;
+            }
             IGX_HIP(ctx, hipGetLastError());
             return IGX_OK;
         }

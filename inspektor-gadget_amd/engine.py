@@ -309,6 +309,13 @@ class Table:
             self.ctx.check(self.ctx.L.igx_groupby_sort(self.h, arr, len(ts), m, ptr(out)))
         return out[:m]
 
+    def topk_counts(self):
+        """igx_groupby_topk_counts (synchronous): (top-Ks answered by the hinted path, by the full
+        selection) so far."""
+        out = (C.c_uint64 * 2)()
+        self.ctx.check(self.ctx.L.igx_groupby_topk_counts(self.h, out))
+        return int(out[0]), int(out[1])
+
     def gather(self, slots):
         """Packed rows (len(slots), key_bytes + 8*naggs + 8) for the given slots."""
         torch = torch_mod()
