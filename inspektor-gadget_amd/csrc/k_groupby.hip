@@ -1981,15 +1981,31 @@ __global__ __launch_bounds__(256) void k_reset_clear(uint32_t *__restrict__ occ,
     if (cont) {
         // one lane per 16-B quad of a record, a record's quads in adjacent lanes: each record
         // leaves as one store instruction's contiguous pieces (one write request per record, the
-        // claim stores' shape), not one request per quad of a lane writing its record alone
+        // claim stores' shape), not one request per quad of a lane writing its record alone.
+        // RU slot-list loads are issued before their stores: one at a time, each store waited
+        // for its own load's round trip and the pass was latency-bound.
+        constexpr int RU = 8;
         const uint64_t ng = *rg.ng;
-        const uint32_t vq = rg.vw == 1 ? 1u : rg.vw / 2;
-        for (uint64_t j = i; j < ng * vq; j += stride) {
-            const uint64_t g = j / vq;
-            const uint32_t q = (uint32_t)(j - g * vq);
-            uint64_t *v = rg.vrec + (uint64_t)rg.groups[g] * rg.vw;
-            if (rg.vw == 1) *v = ~0ull;
-            else reinterpret_cast<uint4 *>(v)[q] = q ? make_uint4(0, 0, 0, 0) : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0);
+        const uint32_t qs = rg.vw == 1 ? 0u : (uint32_t)__builtin_ctz(rg.vw / 2);   // log2 quads per record
+        const uint64_t total = ng << qs;
+        const uint32_t *__restrict__ groups = rg.groups;
+        uint64_t *__restrict__ vrec = rg.vrec;
+        for (uint64_t j0 = i; j0 < total; j0 += RU * stride) {
+            uint32_t slot[RU];
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const uint64_t j = j0 + u * stride;
+                slot[u] = j < total ? groups[j >> qs] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const uint64_t j = j0 + u * stride;
+                if (j >= total) break;
+                const uint32_t q = (uint32_t)(j & ((1ull << qs) - 1));
+                uint64_t *v = vrec + (uint64_t)slot[u] * rg.vw;
+                if (rg.vw == 1) *v = ~0ull;
+                else reinterpret_cast<uint4 *>(v)[q] = q ? make_uint4(0, 0, 0, 0) : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0);
+            }
         }
     }
     if (i == 0) {
@@ -2300,7 +2316,7 @@ extern "C" int igx_groupby_reset(igx_table *t) {
     t->gen_planned = rg.may != 0;
     // the bitmap, the error bits and the LDS-miss count (and the byte map if it holds claims)
     const uint64_t nb16 = t->occb_dirty ? t->occ_words * 2 : 0;
-    const uint64_t grid = rg.may ? 1024 : std::min<uint64_t>(1024, (std::max(t->occ_words / 4, nb16) + 255) / 256 + 1);
+    const uint64_t grid = rg.may ? 2048 : std::min<uint64_t>(1024, (std::max(t->occ_words / 4, nb16) + 255) / 256 + 1);
     hipLaunchKernelGGL(k_reset_clear, dim3((unsigned)grid), dim3(256), 0, ctx->stream, t->occ, t->occ_words, t->err,
                        reinterpret_cast<uint4 *>(t->occb), nb16, rg);
     t->occb_dirty = false;
