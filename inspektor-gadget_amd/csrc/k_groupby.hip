@@ -2584,14 +2584,17 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
                                                             : (size_t)trb * (16 * p.rq + 6) + 12 * (size_t)F2 + 4 * 17;
     const size_t lds_c = (size_t)p.E * entry + 8 * (size_t)p.occw + 16 + stage_c;
     // dynamic LDS granted to each kernel so far; pass C has a distinct-only instantiation
-    static size_t lds_set[5] = {0, 0, 0, 0, 0};
-    const void *kern[5] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
+    constexpr bool PEK = pack_words<L>() <= 3;   // a packed-entry pass C exists for this layout
+    static size_t lds_set[6] = {0, 0, 0, 0, 0, 0};
+    const void *kern[6] = {reinterpret_cast<const void *>(k_gbp_count<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_a<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_b<L, NV>),
                            reinterpret_cast<const void *>(k_gbp_c<L, NV, AMAX>),
-                           reinterpret_cast<const void *>(k_gbp_c<L, NV, 0>)};
-    const size_t need[5] = {lds_k, lds_a, lds_b, t->naggs ? lds_c : 0, t->naggs ? 0 : lds_c};
-    for (int i = 0; i < 5; ++i) {
+                           reinterpret_cast<const void *>(k_gbp_c<L, NV, 0>),
+                           reinterpret_cast<const void *>(k_gbp_c<L, NV, 0, PEK>)};
+    const bool pe_c = PEK && p.pe;
+    const size_t need[6] = {lds_k, lds_a, lds_b, t->naggs ? lds_c : 0, t->naggs || pe_c ? 0 : lds_c, pe_c ? lds_c : 0};
+    for (int i = 0; i < 6; ++i) {
         if (need[i] > lds_set[i]) {
             IGX_HIP(ctx, hipFuncSetAttribute(kern[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need[i]));
             lds_set[i] = need[i];
@@ -2622,7 +2625,9 @@ static int launch_part_as(igx_table *t, igx_ctx *ctx, GbArgs &a, PartArgs &p, bo
     }
     if (t->naggs)
         hipLaunchKernelGGL((k_gbp_c<L, NV, AMAX>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
-    else   // distinct-only (C4): no aggregate decode or accumulate in the per-record path
+    else if (pe_c)   // distinct-only with packed entries (C4)
+        hipLaunchKernelGGL((k_gbp_c<L, NV, 0, PEK>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
+    else   // distinct-only: no aggregate decode or accumulate in the per-record path
         hipLaunchKernelGGL((k_gbp_c<L, NV, 0>), dim3(2 * cus), dim3(PTC), lds_c, ctx->stream, a, p);
     return IGX_OK;
 }

@@ -1122,7 +1122,10 @@ __device__ __forceinline__ void c_row_pe(const GbArgs &a, const PartArgs &p, uin
     }
 }
 
-template <class L, int NV, int NA>
+// PE: the packed-entry instance (c_row_pe; distinct-only, pack_words <= 3) -- its own kernel,
+// so neither instance carries the other's per-record and flush code (registers are allocated
+// over the whole kernel: the two paths together spilled 100-300 SGPRs into VGPR lanes)
+template <class L, int NV, int NA, bool PE = false>
 __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
     constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
@@ -1137,8 +1140,8 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     T.occ_old = T.key + (uint64_t)E * KW;
     T.occ_new = T.occ_old + p.occw;
     T.flag = T.occ_new + p.occw;
-    constexpr bool PEC = NA == 0 && pack_words<L>() <= 3;
-    const bool pe = PEC && p.pe;
+    static_assert(!PE || (NA == 0 && pack_words<L>() <= 3), "packed entries: distinct-only, <= 3 words");
+    constexpr bool pe = PE;
     uint8_t *tg8 = reinterpret_cast<uint8_t *>(lds);     // packed entries: E tag bytes ...
     uint4 *ent = reinterpret_cast<uint4 *>(tg8 + E);      // ... then E 16-B entries
     if (pe) {
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         if (threadIdx.x == 0) T.flag[1] = atomicAdd(&p.ctl[0], 1u);
         for (uint32_t x = threadIdx.x; x < E; x += PTC) {
             if ((x & 3) == 0) reinterpret_cast<uint32_t *>(T.tag)[x >> 2] = 0;
-            if (pe) continue;   // a claim writes its whole entry
+            if constexpr (PE) continue;   // a claim writes its whole entry
             T.first[x] = ~0ull;
             for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
         }
@@ -1190,13 +1193,8 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             for (uint32_t u = 0; u < uc; ++u) {
                 const uint32_t i = u * PTC + threadIdx.x;
                 const uint32_t *rec = reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq);
-                if constexpr (PEC) {
-                    if (pe) {
-                        c_row_pe<L>(a, p, tg8, ent, E, T.flag, r0 + i < e, rec);
-                        continue;
-                    }
-                }
-                c_row<L, NA>(a, p, T, r0 + i < e, rec);
+                if constexpr (PE) c_row_pe<L>(a, p, tg8, ent, E, T.flag, r0 + i < e, rec);
+                else c_row<L, NA>(a, p, T, r0 + i < e, rec);
             }
         }
         __syncthreads();
@@ -1213,18 +1211,16 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         }
         for (uint32_t x = threadIdx.x; x < E && !(p.dbg & 16u); x += PTC) {
             if (!(T.tag[x] & 0x80u)) continue;
-            if constexpr (PEC) {
-                if (pe) {
-                    const uint4 q = ent[x];
-                    const uint32_t w4[4] = {q.x, q.y, q.z, 0u};
-                    uint32_t k[KW];
-                    lds_key<L>(p, w4, k);
-                    const uint64_t v[1] = {0};
-                    const uint64_t h = hash_key<KW>(k), f = a.base_idx + q.w;
-                    if (owned) flush_owned<KW, 1>(a, T, k, h, v, f, sb, p.sb_log);
-                    else hbm_merge<KW, 1>(a, k, h, v, f);
-                    continue;
-                }
+            if constexpr (PE) {
+                const uint4 q = ent[x];
+                const uint32_t w4[4] = {q.x, q.y, q.z, 0u};
+                uint32_t k[KW];
+                lds_key<L>(p, w4, k);
+                const uint64_t v[1] = {0};
+                const uint64_t h = hash_key<KW>(k), f = a.base_idx + q.w;
+                if (owned) flush_owned<KW, 1>(a, T, k, h, v, f, sb, p.sb_log);
+                else hbm_merge<KW, 1>(a, k, h, v, f);
+                continue;
             }
             uint32_t k[KW];
 #pragma unroll

@@ -1013,14 +1013,14 @@ static int np_pod_labels(u32 id, const char *app_prefix, int with_tier, np_label
     return n;
 }
 
-static int np_local_pod_key(u32 s, char *out) {   /* localPodKey, advisor.go:143-145 */
+static int np_local_pod_key(u32 s, char *out) {   /* localPodKey, advisor.go:146-148 */
     np_label L[4];
     const int nl = np_pod_labels(s, "app", 1, L);
     int len = sprintf(out, "ns-%u:", s % 50);
     return len + np_label_key_string(L, nl, out + len);
 }
 
-static int np_peer_key(u32 p, u16 port, char *out) {   /* networkPeerKey, advisor.go:147-158 */
+static int np_peer_key(u32 p, u16 port, char *out) {   /* networkPeerKey, advisor.go:150-159 */
     char ret[160];
     int len;
     if (p % 3 == 0 || p % 3 == 1) {   /* RemoteKindPod / RemoteKindService */
