@@ -1125,13 +1125,15 @@ __device__ __forceinline__ void c_row_pe(const GbArgs &a, const PartArgs &p, uin
 // PE: the packed-entry instance (c_row_pe; distinct-only, pack_words <= 3) -- its own kernel,
 // so neither instance carries the other's per-record and flush code (registers are allocated
 // over the whole kernel: the two paths together spilled 100-300 SGPRs into VGPR lanes)
-template <class L, int NV, int NA, bool PE = false>
-__global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
+// TPB: threads per block (PTC: two 80 KB blocks per CU; one 1 024-thread block over the whole
+// 160 KB -- half the buckets -- measured slower, DESIGN.md §4 "Round 6: pass C")
+template <class L, int NV, int NA, bool PE = false, int TPB = PTC>
+__global__ __launch_bounds__(TPB) void k_gbp_c(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
     constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
     extern __shared__ uint64_t lds[];
     AggTab<KW> T;
-    const uint32_t E = p.E, rq = p.rq, uc = p.uc, RC = uc * PTC;
+    const uint32_t E = p.E, rq = p.rq, uc = p.uc, RC = uc * TPB;
     T.E = E;
     T.first = lds;
     T.agg = lds + E;
@@ -1155,13 +1157,16 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
     const uint32_t nitems = p.ctl[2];
     for (;;) {
         if (threadIdx.x == 0) T.flag[1] = atomicAdd(&p.ctl[0], 1u);
-        for (uint32_t x = threadIdx.x; x < E; x += PTC) {
-            if ((x & 3) == 0) reinterpret_cast<uint32_t *>(T.tag)[x >> 2] = 0;
-            if constexpr (PE) continue;   // a claim writes its whole entry
-            T.first[x] = ~0ull;
-            for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
+        if constexpr (PE) {   // only the tags (a claim writes its whole entry): 16 per store
+            for (uint32_t q = threadIdx.x; q < E / 16; q += TPB) reinterpret_cast<uint4 *>(tg8)[q] = make_uint4(0, 0, 0, 0);
+        } else {
+            for (uint32_t x = threadIdx.x; x < E; x += TPB) {
+                if ((x & 3) == 0) reinterpret_cast<uint32_t *>(T.tag)[x >> 2] = 0;
+                T.first[x] = ~0ull;
+                for (uint32_t g = 0; g < a.naggs; ++g) T.agg[(uint64_t)g * E + x] = 0;
+            }
         }
-        if (threadIdx.x == 0) T.flag[0] = 0;
+        if (threadIdx.x == 0) T.flag[0] = T.flag[2] = 0;
         __syncthreads();
         const uint32_t it = T.flag[1];
         if (it >= nitems) break;
@@ -1178,7 +1183,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         auto prefetch = [&](uint32_t r0) {
 #pragma unroll
             for (uint32_t m = 0; m < UCMAX * QM; ++m)
-                if (m < mq) pf[m] = __builtin_nontemporal_load(recs + min((uint64_t)r0 * rq + m * PTC + threadIdx.x, qlast));
+                if (m < mq) pf[m] = __builtin_nontemporal_load(recs + min((uint64_t)r0 * rq + m * TPB + threadIdx.x, qlast));
         };
         if (s < e && !(p.dbg & 8u)) prefetch(s);
         for (uint32_t r0 = s; r0 < e && !(p.dbg & 8u); r0 += RC) {
@@ -1186,12 +1191,12 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
             __syncthreads();   // the previous round's records are no longer read
 #pragma unroll
             for (uint32_t m = 0; m < UCMAX * QM; ++m)
-                if (m < mq && m * PTC + threadIdx.x < nq)
-                    stage[m * PTC + threadIdx.x] = make_uint4(pf[m].x, pf[m].y, pf[m].z, pf[m].w);
+                if (m < mq && m * TPB + threadIdx.x < nq)
+                    stage[m * TPB + threadIdx.x] = make_uint4(pf[m].x, pf[m].y, pf[m].z, pf[m].w);
             __syncthreads();
             if (r0 + RC < e) prefetch(r0 + RC);
             for (uint32_t u = 0; u < uc; ++u) {
-                const uint32_t i = u * PTC + threadIdx.x;
+                const uint32_t i = u * TPB + threadIdx.x;
                 const uint32_t *rec = reinterpret_cast<const uint32_t *>(stage + (uint64_t)min(i, RC - 1) * rq);
                 if constexpr (PE) c_row_pe<L>(a, p, tg8, ent, E, T.flag, r0 + i < e, rec);
                 else c_row<L, NA>(a, p, T, r0 + i < e, rec);
@@ -1203,14 +1208,36 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         const bool owned = nit == 1 && T.flag[0] == 0;
         const uint64_t sb = (uint64_t)fb << p.sb_log;
         if (owned) {
-            for (uint32_t i = threadIdx.x; i < p.occw; i += PTC) {
+            for (uint32_t i = threadIdx.x; i < p.occw; i += TPB) {
                 T.occ_old[i] = a.occ[(sb >> 5) + i];
                 T.occ_new[i] = 0;
             }
             __syncthreads();
         }
-        for (uint32_t x = threadIdx.x; x < E && !(p.dbg & 16u); x += PTC) {
-            if (!(T.tag[x] & 0x80u)) continue;
+        // About a quarter of the entries hold a group, so a loop over the entries ran the flush
+        // with a quarter of each wave's lanes busy, once per TPB entries: the live entries are
+        // first listed densely (16-bit ids in the stage buffer, free after the last round; one
+        // LDS atomic per wave and pass), so every lane flushes a group.  A stage buffer smaller
+        // than 2 E bytes (IGX_GBP_UC=1 on one-quad records) keeps the loop over the entries.
+        const bool dense = 2u * E <= RC * rq * 16u && !(p.dbg & 2048u);
+        uint16_t *live = reinterpret_cast<uint16_t *>(stage);
+        if (dense && !(p.dbg & 16u)) {
+            const uint32_t lane = threadIdx.x & 63;
+            for (uint32_t x0 = 0; x0 < E; x0 += TPB) {
+                const uint32_t x = x0 + threadIdx.x;
+                const bool lv = x < E && (T.tag[x] & 0x80u);
+                const uint64_t b = __ballot(lv);
+                uint32_t base = 0;
+                if (lane == 0 && b) base = atomicAdd(&T.flag[2], (uint32_t)__popcll(b));
+                base = __shfl(base, 0);
+                if (lv) live[base + (uint32_t)__popcll(b & ((1ull << lane) - 1))] = (uint16_t)x;
+            }
+            __syncthreads();
+        }
+        const uint32_t nflush = dense ? T.flag[2] : E;
+        for (uint32_t i = threadIdx.x; i < nflush && !(p.dbg & 16u); i += TPB) {
+            const uint32_t x = dense ? live[i] : i;
+            if (!dense && !(T.tag[x] & 0x80u)) continue;
             if constexpr (PE) {
                 const uint4 q = ent[x];
                 const uint32_t w4[4] = {q.x, q.y, q.z, 0u};
@@ -1235,7 +1262,7 @@ __global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
         }
         __syncthreads();
         if (owned) {
-            for (uint32_t i = threadIdx.x; i < p.occw; i += PTC)
+            for (uint32_t i = threadIdx.x; i < p.occw; i += TPB)
                 if (T.occ_new[i]) a.occ[(sb >> 5) + i] = T.occ_old[i] | T.occ_new[i];
             __syncthreads();
         }

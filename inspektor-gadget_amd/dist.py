@@ -118,13 +118,17 @@ class IgxComm:
         t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=dev)
         d.broadcast(t, 0)
         v = t.cpu().tolist()
+        # every rank's status, before any rank enters igx_dist_init: a rank that cannot open the
+        # transport would otherwise leave its peers inside ncclCommInitRank until the deadline
+        # (IGX_DIST_TIMEOUT_MS) -- now all of them raise here and select_transport falls back
+        st = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=dev)
+        d.all_reduce(st, op=d.ReduceOp.MIN)
         if err is not None:
-            # this rank cannot open the transport; its peers, already past the broadcast, fail
-            # igx_dist_init within IGX_DIST_TIMEOUT_MS, and select_transport's all-reduce then
-            # moves every rank to the fallback
             raise RuntimeError(f"IgxComm on rank {rank}: {err}")
         if not v[-1]:
             raise RuntimeError("igx_dist_get_unique_id failed on rank 0")
+        if int(st.item()) == 0:
+            raise RuntimeError(f"IgxComm on rank {rank}: a peer could not open the transport")
         uid = (C.c_uint8 * _abi.DIST_ID_BYTES)(*v[:-1])
         h = C.c_void_p()
         self.ctx.check(self.ctx.L.igx_dist_init(self.ctx.h, uid, ws, rank, C.byref(h)))
