@@ -287,17 +287,23 @@ def exchange_rows(rows, key_bytes):
 def unpack_rows(rows, key_widths, naggs):
     """Packed group rows (key padded to 4-byte columns | naggs x u64 | first u64) -> SoA
     tensors: key columns (u8 (n, w) for byte keys, typed for 1/2/4/8), aggregates, first."""
+    from . import engine
     torch = torch_mod()
     typed = {1: torch.uint8, 2: torch.uint16, 4: torch.uint32, 8: torch.uint64}
-    cols, o = [], 0
-    for w in key_widths:
-        c = rows[:, o:o + w].contiguous()
-        cols.append(c.view(typed[w]).flatten() if w in typed else c)
+    fields, o = [], 0
+    for i, w in enumerate(key_widths):
+        fields.append((i, o, w, typed.get(w)))
         o += (w + 3) // 4 * 4
-    aggs = [rows[:, o + 8 * x:o + 8 * x + 8].contiguous().view(torch.uint64).flatten()
-            for x in range(naggs)]
-    first = rows[:, o + 8 * naggs:o + 8 * naggs + 8].contiguous().view(torch.uint64).flatten()
-    return cols, aggs, first
+    nk = len(key_widths)
+    fields += [(nk + x, o + 8 * x, 8, torch.uint64) for x in range(naggs + 1)]
+    # the rows cut into columns in one pass on the device (igx_ingest_aos, the wire-format
+    # ingest's kernel), not one strided torch copy per field, each re-reading every row
+    r8 = rows.contiguous().view(torch.uint8)   # (n, row bytes)
+    cols = {}
+    for f0 in range(0, len(fields), 16):   # igx_ingest_aos takes up to 16 fields a call
+        cols.update(engine.ingest_aos(r8, r8.shape[0], r8.shape[1], fields[f0:f0 + 16]))
+    outs = [cols[i] for i in range(len(fields))]
+    return outs[:nk], outs[nk:nk + naggs], outs[nk + naggs]
 
 
 def owner_table(key_widths, out_widths, capacity):

@@ -541,7 +541,7 @@ def test_direct_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layou
     tab.destroy()
 
 
-@pytest.mark.parametrize("variant", ["plain", "skewed", "lds_overflow", "index_column", "region", "region_overflow"])
+@pytest.mark.parametrize("variant", ["plain", "skewed", "lds_overflow", "index_column", "region", "region_overflow", "uc1"])
 @pytest.mark.parametrize("layout", ["tcp", "file", "np_distinct", "generic"])
 def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, layout, variant):
     """IGX_GB_PART (k_groupby_part.h: count, scan, scatter into hash buckets, LDS aggregation
@@ -553,7 +553,9 @@ def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, 
     global indices from a u64 column (the owner-side merge of igx_dist_exchange_groups).
     'region' / 'region_overflow': the region variant AUTO runs (no count pass, buckets filled
     through cursors), the second with regions of 600 records so that most records take the
-    direct find-or-insert path from passes A and B."""
+    direct find-or-insert path from passes A and B.  'uc1': one record per thread and round in
+    pass C (IGX_GBP_UC=1), whose stage buffer is then too small for the dense list of live
+    entries on one-quad records, so pass C's flush takes its loop over all entries."""
     A = igx._abi
     if variant.startswith("region"):
         monkeypatch.setenv("IGX_GBP_REGION", "1")
@@ -592,6 +594,8 @@ def test_partitioned_form_matches_oracle(oracle, E, H, igx, torch, monkeypatch, 
         oaggs = [{"kind": "sum", "val": ev_h["size"]}]
     if variant == "lds_overflow":
         monkeypatch.setenv("IGX_GBP_ENTRIES", "8")
+    if variant == "uc1":
+        monkeypatch.setenv("IGX_GBP_UC", "1")
     valid = (rng.random(n) > 0.05).astype(np.uint8)
     ev = {k: H.to_device(v) for k, v in ev_h.items()}
     cols = [ev[k] for k in names + extra]

@@ -145,3 +145,28 @@ def test_bench_transport_check_single_rank(igx, torch):
         ctx["igx_comm"].close()
     finally:
         dist.destroy_process_group()
+
+
+
+@pytest.mark.parametrize("layout", ["c5", "c2", "c4"])
+def test_unpack_rows_matches_slicing(igx, torch, layout):
+    """dist.unpack_rows (the owner merge's exchanged rows -> the SoA columns the update reads,
+    one igx_ingest_aos pass) equals slicing every field out of the rows on the host -- key
+    columns padded to 4 bytes, then the u64 aggregates and first index -- for C5's, C2's and C4's
+    rows, including zero rows."""
+    D = importlib.import_module("inspektor-gadget_amd.dist")
+    widths, naggs = {"c5": ([8, 4, 4, 4], 4), "c2": ([16, 16, 8, 4, 16, 2, 2, 2], 2), "c4": ([4, 1, 4, 2], 0)}[layout]
+    offs, o = [], 0
+    for w in widths:
+        offs.append(o)
+        o += (w + 3) // 4 * 4
+    rb = o + 8 * (naggs + 1)
+    rng = np.random.default_rng(rb)
+    for n in (0, 1, 1000, 300_001):
+        h = rng.integers(0, 256, size=(n, rb), dtype=np.uint8)
+        kcols, aggs, first = D.unpack_rows(igx.columns.to_device(h), widths, naggs)
+        got = [(t, ko, w) for t, ko, w in zip(kcols, offs, widths)]
+        got += [(t, o + 8 * x, 8) for x, t in enumerate(aggs + [first])]
+        for t, fo, w in got:
+            b = t.view(torch.uint8).cpu().numpy().reshape(n, w)
+            assert np.array_equal(b, h[:, fo:fo + w]), (layout, n, fo, w)
