@@ -2733,14 +2733,17 @@ static int launch_part(igx_table *t, igx_ctx *ctx, GbArgs &a) {
 // interval's cached updates adopts the found ones before its stream starts.  Hot keys of a
 // stream are stable, so the seeds are recomputed every SEED_EVERY seeded intervals (and after a
 // generation ended); seeds of another generation are never adopted (the kernel compares).
-constexpr uint32_t SEED_EVERY = 8;
+constexpr uint32_t SEED_EVERY = 16;   // round 6: 8 -> 16 and rows / 64 -> rows / 128 (profiles/r06/seed_period_ab.txt)
 constexpr uint64_t SEED_MIN_ROWS = 8u << 20;    // smaller updates: no seeds (IGX_GB_SEED_MIN overrides)
-constexpr uint64_t SEED_SAMPLE = 1u << 20;      // sampled rows: max(1M, rows / 64)
+constexpr uint64_t SEED_SAMPLE = 1u << 20;      // sampled rows: max(1M, rows / SEED_DIV)
+constexpr uint64_t SEED_DIV = 128;
 
 template <class L>
 static int seeds_compute_static(igx_table *t, igx_ctx *ctx, const GbArgs &a) {
     const uint32_t E = gb_entries_for<L>(t->naggs);
-    const uint64_t S = std::min<uint64_t>(a.n, std::max<uint64_t>(SEED_SAMPLE, a.n / 64));
+    uint64_t div = SEED_DIV;
+    if (const char *d = std::getenv("IGX_GB_SEED_DIV")) div = std::max<uint64_t>(1, std::strtoull(d, nullptr, 0));   // A/B knob
+    const uint64_t S = std::min<uint64_t>(a.n, std::max<uint64_t>(SEED_SAMPLE, a.n / div));
     if (t->seed_tab && t->seed_tab->cap < S) {
         igx_groupby_destroy(t->seed_tab);
         t->seed_tab = nullptr;
@@ -2867,7 +2870,10 @@ static int launch_form(igx_table *t, igx_ctx *ctx, GbArgs &a, uint32_t blocks) {
             t->interval_seeded = false;
             if (L::is_static && t->seed_on && t->gen_planned && !a.dbg && a.n >= min_rows) {
                 if (t->seed_left == 0 || !t->nseeds) {
-                    if (seeds_compute<L>(t, ctx, a) == IGX_OK) t->seed_left = SEED_EVERY;
+                    uint32_t every = SEED_EVERY;
+                    if (const char *e = std::getenv("IGX_GB_SEED_EVERY"))   // A/B knob
+                        every = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 0));
+                    if (seeds_compute<L>(t, ctx, a) == IGX_OK) t->seed_left = every;
                     else t->nseeds = 0;   // no seeds this time (the sample table failed): plain cache
                 }
                 --t->seed_left;

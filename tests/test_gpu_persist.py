@@ -227,12 +227,13 @@ def test_top_tcp_rotating_batches(igx, torch, oracle):
 @pytest.mark.parametrize("prober", ["0", "1"])
 def test_seeded_cache_exact(igx, torch, oracle, monkeypatch, prober):
     """The sample-seeded LDS cache (IGX_GB_SEED_MIN=1: every interval of these small streams is
-    seeded; the seeds are recomputed every 8 intervals, so most intervals adopt seeds counted
+    seeded; IGX_GB_SEED_EVERY=4: the seeds are recomputed every 4 intervals, so most adopt seeds counted
     on an earlier interval's rows -- keys that moved out of the window are simply not found).
     A seeded key may see only LDS hits in an interval: its group must still be listed, with its
     sums and first index, and its `ready` is never re-stamped.  Every interval against the
     oracle; the claims model still holds (seeds are never inserted)."""
     monkeypatch.setenv("IGX_GB_SEED_MIN", "1")
+    monkeypatch.setenv("IGX_GB_SEED_EVERY", "4")
     monkeypatch.setenv("IGX_GB_PROBER", prober)
     rng = np.random.default_rng(0x5EED + int(prober))
     U = _universe(150_000)
