@@ -519,6 +519,17 @@ __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p,
 // The tile's rows stay in registers (R per thread, all loads issued at once); a row's rank
 // in its bucket comes from an LDS atomic, so the records are staged in LDS already sorted
 // and leave as whole runs, 16 B per lane.
+// a partition pass's record store, written once and read back only by the next pass.  Pass
+// B's are non-temporal: its runs (~48 records) fill whole lines, and on C4 pass B took 1 % less
+// and pass C, which no longer finds L2 full of B's dirty lines, 6 % less
+// (profiles/r06/part_stnt_ab.txt).  Pass A's stay plain: non-temporal, A took 14 % more (its
+// runs into the first-level regions leave partial lines that L2 merges).
+template <bool NT>
+__device__ __forceinline__ void st_rec(uint4 *p, const uint4 q) {
+    if constexpr (NT) __builtin_nontemporal_store(u4v{q.x, q.y, q.z, q.w}, reinterpret_cast<u4v *>(p));
+    else *p = q;
+}
+
 template <class L, int NV>
 __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
@@ -583,8 +594,8 @@ __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
         const uint32_t g = base[b] + j - off[b];
         bool spill = false;
         if (!live) {
-        } else if (!p.reg1) out[(uint64_t)g * rq + q] = stage[qi];
-        else if (g < p.reg1) out[((uint64_t)((b << p.s1log) + sl) * p.reg1 + g) * rq + q] = stage[qi];
+        } else if (!p.reg1) st_rec<false>(&out[(uint64_t)g * rq + q], stage[qi]);
+        else if (g < p.reg1) st_rec<false>(&out[((uint64_t)((b << p.s1log) + sl) * p.reg1 + g) * rq + q], stage[qi]);
         else spill = q == 0;
         if (p.reg1) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? j : 0u) * rq));
     }
@@ -720,8 +731,8 @@ __device__ __forceinline__ void gbp_b_run(const GbArgs &a, const PartArgs &p, ui
         const uint32_t g = base[b] + jj - off[b];
         bool spill = false;
         if (!live) {
-        } else if (!p.reg2) out[(uint64_t)g * RQ + q] = stage[qi];
-        else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * RQ + q] = stage[qi];
+        } else if (!p.reg2) st_rec<true>(&out[(uint64_t)g * RQ + q], stage[qi]);
+        else if (g < p.reg2) st_rec<true>(&out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * RQ + q], stage[qi]);
         else spill = q == 0;
         if (p.reg2) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)(live ? jj : 0u) * RQ));
     }
@@ -799,8 +810,8 @@ __global__ __launch_bounds__(PTA) void k_gbp_b(GbArgs a, PartArgs p) {
         const uint32_t g = base[b] + jj - off[b];
         bool spill = false;
         if (!live) {
-        } else if (!p.reg2) out[(uint64_t)g * rq + q] = stage[sidx * rq + q];
-        else if (g < p.reg2) out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * rq + q] = stage[sidx * rq + q];
+        } else if (!p.reg2) st_rec<true>(&out[(uint64_t)g * rq + q], stage[sidx * rq + q]);
+        else if (g < p.reg2) st_rec<true>(&out[((uint64_t)((b1 << p.f2) + b) * p.reg2 + g) * rq + q], stage[sidx * rq + q]);
         else spill = q == 0;
         if (p.reg2) region_spill<L>(a, p, spill, reinterpret_cast<const uint32_t *>(stage + (uint64_t)sidx * rq));
     }
