@@ -390,6 +390,9 @@ def test_netpolicy_mark_and_masked_distinct(oracle, E, H, igx, torch):
     # columns at an offset (u8 columns 4-B but not 16-B aligned)
     keep4 = E.np_mark(ev["type"][4:], ev["pkt"][4:], ev["hostip"][4:], ev["raddr"][4:])
     assert np.array_equal(H.host(keep4).astype(bool), ref_keep[4:])
+    for m in (1, 3, 4, 5, 7, 1027):   # fewer rows than one quad, and a few quads with a tail
+        km = E.np_mark(ev["type"][:m], ev["pkt"][:m], ev["hostip"][:m], ev["raddr"][:m])
+        assert np.array_equal(H.host(km).astype(bool), ref_keep[:m]), m
     names = ("src", "pkt", "peer", "port")
     tab = E.Table([4, 1, 4, 2], [A.Agg(A.AGG_COUNT, 0, A.NO_COL, 8, 0)], n)
     tab.update([ev[k] for k in names], [0, 1, 2, 3], n, 17, valid=keep)
