@@ -515,10 +515,6 @@ __device__ __forceinline__ void region_spill(const GbArgs &a, const PartArgs &p,
     if (lead) hbm_merge<KW, AMAX>(a, k, h, v, gidx);
 }
 
-// ---- A: a tile of rows -> records, each first-level bucket's run at its exact position -----
-// The tile's rows stay in registers (R per thread, all loads issued at once); a row's rank
-// in its bucket comes from an LDS atomic, so the records are staged in LDS already sorted
-// and leave as whole runs, 16 B per lane.
 // a partition pass's record store, written once and read back only by the next pass.  Pass
 // B's are non-temporal: its runs (~48 records) fill whole lines, and on C4 pass B took 1 % less
 // and pass C, which no longer finds L2 full of B's dirty lines, 6 % less
@@ -530,6 +526,10 @@ __device__ __forceinline__ void st_rec(uint4 *p, const uint4 q) {
     else *p = q;
 }
 
+// ---- A: a tile of rows -> records, each first-level bucket's run at its exact position -----
+// The tile's rows stay in registers (R per thread, all loads issued at once); a row's rank
+// in its bucket comes from an LDS atomic, so the records are staged in LDS already sorted
+// and leave as whole runs, 16 B per lane.
 template <class L, int NV>
 __global__ __launch_bounds__(PTA) void k_gbp_a(GbArgs a, PartArgs p) {
     constexpr int KW = L::KW;
@@ -1135,11 +1135,12 @@ __device__ __forceinline__ void c_row_pe(const GbArgs &a, const PartArgs &p, uin
 
 // PE: the packed-entry instance (c_row_pe; distinct-only, pack_words <= 3) -- its own kernel,
 // so neither instance carries the other's per-record and flush code (registers are allocated
-// over the whole kernel: the two paths together spilled 100-300 SGPRs into VGPR lanes)
-// TPB: threads per block (PTC: two 80 KB blocks per CU; one 1 024-thread block over the whole
-// 160 KB -- half the buckets -- measured slower, DESIGN.md §4 "Round 6: pass C")
-template <class L, int NV, int NA, bool PE = false, int TPB = PTC>
-__global__ __launch_bounds__(TPB) void k_gbp_c(GbArgs a, PartArgs p) {
+// over the whole kernel: the two paths together spilled 100-300 SGPRs into VGPR lanes).
+// Two 80 KB blocks of PTC threads per CU (one 1 024-thread block over the whole 160 KB, half
+// the buckets, measured slower: DESIGN.md §4 "Round 6: pass C").
+template <class L, int NV, int NA, bool PE = false>
+__global__ __launch_bounds__(PTC) void k_gbp_c(GbArgs a, PartArgs p) {
+    constexpr uint32_t TPB = PTC;
     constexpr int KW = L::KW;
     constexpr int QM = part_w<KW, NV>() / 4;   // quads per record, compile-time bound
     extern __shared__ uint64_t lds[];
